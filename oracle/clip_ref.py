@@ -1,0 +1,214 @@
+"""CPU oracle for the CLIP dual-encoder + adapter contrastive step.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the checker /
+CPU baseline.  The product path (``vlm-clip_amd/clipmi``) never imports it.
+
+This is a plain PyTorch-CPU restatement (fp32 by default, fp64 on request) of the math
+the reference runs through HF transformers + its own modules.  Every function cites the
+reference line it follows.  HF transformers is a third-party dependency of the reference
+(pinned 4.51.3 at ``uv.lock:1540-1541``; not vendored under /root/reference); its CLIP
+math is restated here from the published source (``[HF] models/clip/modeling_clip.py``,
+installed copy 5.15.0).
+
+Pinning: ``tests/golden/*.npz`` were produced by importing the reference's own
+``model_m.CLIPWithAdapters`` / ``adapter.clip_adapter`` in the build container
+(``tools/gen_goldens.py``); ``tests/test_oracle_golden.py`` checks this restatement
+against them.  The reference ships no numeric fixtures of its own.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def layer_norm(x, w, b, eps):
+    # nn.LayerNorm(eps=config.layer_norm_eps)  [HF] modeling_clip.py:357,359
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+def quick_gelu(x):
+    # [HF] activations.py:117-123: x * sigmoid(1.702 x)
+    return x * torch.sigmoid(1.702 * x)
+
+
+def gelu_erf(x):
+    # nn.GELU() default (approximate='none'), adapter/clip_adapter.py:13,140
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+
+def linear(x, w, b=None):
+    y = x @ w.t()
+    return y if b is None else y + b
+
+
+def attention(x, p, prefix, heads, mask):
+    """CLIPAttention.forward + eager_attention_forward, [HF] modeling_clip.py:259-335."""
+    B, N, D = x.shape
+    hd = D // heads
+    q = linear(x, p[f"{prefix}.q_proj.weight"], p[f"{prefix}.q_proj.bias"])
+    k = linear(x, p[f"{prefix}.k_proj.weight"], p[f"{prefix}.k_proj.bias"])
+    v = linear(x, p[f"{prefix}.v_proj.weight"], p[f"{prefix}.v_proj.bias"])
+    q, k, v = (t.view(B, N, heads, hd).transpose(1, 2) for t in (q, k, v))
+    s = (q @ k.transpose(-1, -2)) * hd ** -0.5            # :268
+    if mask is not None:
+        s = s + mask                                         # :269-270
+    pr = torch.softmax(s, dim=-1)                            # :271 (fp32 softmax)
+    o = (pr @ v).transpose(1, 2).reshape(B, N, D)           # :274-275, :331
+    return linear(o, p[f"{prefix}.out_proj.weight"], p[f"{prefix}.out_proj.bias"])
+
+
+def encoder_layer(x, p, prefix, heads, eps, mask):
+    """CLIPEncoderLayer.forward, [HF] modeling_clip.py:362-383 (pre-LN, two residuals)."""
+    h = layer_norm(x, p[f"{prefix}.layer_norm1.weight"], p[f"{prefix}.layer_norm1.bias"], eps)
+    x = x + attention(h, p, f"{prefix}.self_attn", heads, mask)
+    h = layer_norm(x, p[f"{prefix}.layer_norm2.weight"], p[f"{prefix}.layer_norm2.bias"], eps)
+    h = linear(h, p[f"{prefix}.mlp.fc1.weight"], p[f"{prefix}.mlp.fc1.bias"])   # :346-350
+    h = quick_gelu(h)
+    h = linear(h, p[f"{prefix}.mlp.fc2.weight"], p[f"{prefix}.mlp.fc2.bias"])
+    return x + h
+
+
+def causal_padding_mask(attention_mask, dtype):
+    """Additive [B,1,N,N] mask: causal + key padding ([HF] modeling_clip.py:543-548)."""
+    B, N = attention_mask.shape
+    neg = torch.finfo(dtype).min
+    causal = torch.triu(torch.ones(N, N, dtype=torch.bool), diagonal=1)
+    keypad = attention_mask[:, None, None, :] == 0
+    blocked = causal[None, None] | keypad
+    return torch.zeros(B, 1, N, N, dtype=dtype).masked_fill(blocked, neg)
+
+
+def text_tower(input_ids, attention_mask, p, cfg):
+    """CLIPTextModel.forward → last_hidden_state (after final_layer_norm), [HF] :513-559."""
+    t = cfg.text_config
+    if input_ids.shape[-1] > t.max_position_embeddings:
+        raise ValueError("Sequence length must be less than max_position_embeddings")
+    pre = "text_model"
+    dt = p[f"{pre}.embeddings.token_embedding.weight"].dtype
+    x = p[f"{pre}.embeddings.token_embedding.weight"][input_ids]                   # :252
+    x = x + p[f"{pre}.embeddings.position_embedding.weight"][: input_ids.shape[1]]  # :254-255
+    mask = causal_padding_mask(attention_mask, dt)
+    for i in range(t.num_hidden_layers):
+        x = encoder_layer(x, p, f"{pre}.encoder.layers.{i}", t.num_attention_heads, t.layer_norm_eps, mask)
+    return layer_norm(x, p[f"{pre}.final_layer_norm.weight"], p[f"{pre}.final_layer_norm.bias"], t.layer_norm_eps)
+
+
+def patch_embed(pixel_values, p, cfg):
+    """CLIPVisionEmbeddings.forward, [HF] :202-218: conv(k=s=P, no bias), CLS, +pos."""
+    v = cfg.vision_config
+    B, C, H, W = pixel_values.shape
+    if H != v.image_size or W != v.image_size:
+        raise ValueError(f"Input image size ({H}*{W}) doesn't match model ({v.image_size}*{v.image_size}).")
+    pre = "vision_model.embeddings"
+    w = p[f"{pre}.patch_embedding.weight"]
+    x = F.conv2d(pixel_values.to(w.dtype), w, stride=v.patch_size)      # :211
+    x = x.flatten(2).transpose(1, 2)                                        # :212
+    cls = p[f"{pre}.class_embedding"].expand(B, 1, -1)                     # :214
+    x = torch.cat([cls, x], dim=1)
+    return x + p[f"{pre}.position_embedding.weight"][None]                # :219
+
+
+def vision_tower(pixel_values, p, cfg):
+    """CLIPVisionModel.forward → last_hidden_state (NO post_layernorm), [HF] :638-651."""
+    v = cfg.vision_config
+    x = patch_embed(pixel_values, p, cfg)
+    x = layer_norm(x, p["vision_model.pre_layrnorm.weight"], p["vision_model.pre_layrnorm.bias"], v.layer_norm_eps)
+    for i in range(v.num_hidden_layers):
+        x = encoder_layer(x, p, f"vision_model.encoder.layers.{i}", v.num_attention_heads, v.layer_norm_eps, None)
+    return x
+
+
+def adapter(x, a, layer_norm_on=True, eps=1e-5):
+    """TextAdapter/VisionAdapter.forward (adapter/clip_adapter.py:17-23, 144-150):
+    LN(up(GELU(down(x))) + x).  With ``layer_norm_on=False`` this is peclip.TextualAdapter
+    (adapter/peclip.py:13-18): up(GELU(down(x))) + x."""
+    h = linear(x, a["down_project.weight"], a["down_project.bias"])
+    h = gelu_erf(h)
+    h = linear(h, a["up_project.weight"], a["up_project.bias"])
+    h = h + x
+    if layer_norm_on:
+        h = layer_norm(h, a["layer_norm.weight"], a["layer_norm.bias"], eps)
+    return h
+
+
+def text_features(input_ids, attention_mask, p, cfg, text_adapter=None, pooling="first"):
+    """CLIPWithAdapters.get_text_features, model_m.py:77-105.
+
+    pooling="first" reproduces ``text_features[:, 0, :]`` (model_m.py:102, quirk Q1);
+    pooling="eos" is HF CLIPTextModel's pooler ([HF] :561-581)."""
+    h = text_tower(input_ids, attention_mask, p, cfg)
+    if text_adapter is not None:
+        h = adapter(h, text_adapter)                                          # :88-90
+    if pooling == "first":
+        pooled = h[:, 0, :]
+    else:
+        eos = cfg.text_config.eos_token_id
+        if eos == 2:
+            idx = input_ids.to(torch.int).argmax(dim=-1)
+        else:
+            idx = (input_ids.to(torch.int) == eos).int().argmax(dim=-1)
+        pooled = h[torch.arange(h.shape[0]), idx]
+    return linear(pooled, p["text_projection.weight"])                      # :103
+
+
+def image_features(pixel_values, p, cfg, vision_adapter=None):
+    """CLIPWithAdapters.get_image_features, model_m.py:107-125 (quirk Q2: no post-LN)."""
+    h = vision_tower(pixel_values, p, cfg)
+    if vision_adapter is not None:
+        h = adapter(h, vision_adapter)                                        # :117-118
+    return linear(h[:, 0, :], p["visual_projection.weight"])                # :122-123
+
+
+def contrastive(text_feat, image_feat, logit_scale):
+    """CLIPWithAdapters.forward contrastive branch, model_m.py:146-171."""
+    t = text_feat / text_feat.norm(dim=-1, keepdim=True)                     # :148
+    i = image_feat / image_feat.norm(dim=-1, keepdim=True)                   # :149
+    lpt = (t @ i.t()) * logit_scale.exp()                                    # :152-155
+    lpi = lpt.t()                                                            # :156
+    labels = torch.arange(t.shape[0])
+    loss = (F.cross_entropy(lpt, labels) + F.cross_entropy(lpi, labels)) / 2  # :159-163
+    return {"loss": loss, "text_features": t, "image_features": i,
+            "logits_per_text": lpt, "logits_per_image": lpi}
+
+
+def clip_with_adapters_forward(batch, p, cfg, text_adapter=None, vision_adapter=None,
+                               return_loss=True, pooling="first"):
+    """CLIPWithAdapters.forward, model_m.py:127-176 (shared adapters off, quirk Q3)."""
+    tf = text_features(batch["input_ids"], batch["attention_mask"], p, cfg, text_adapter, pooling)
+    imf = image_features(batch["pixel_values"], p, cfg, vision_adapter)
+    if return_loss:
+        return contrastive(tf, imf, p["logit_scale"])
+    return {"text_features": tf, "image_features": imf}
+
+
+def to_torch(sd, dtype=torch.float32, requires_grad=False):
+    out = {}
+    for k, v in sd.items():
+        t = torch.as_tensor(v).to(dtype).clone()
+        t.requires_grad_(requires_grad)
+        out[k] = t
+    return out
+
+
+def adamw_reference(params, grads, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.01):
+    """torch.optim.AdamW single step restated (decoupled weight decay), trainer.py:46-48,98."""
+    out = []
+    for p, g, mm, vv in zip(params, grads, m, v):
+        p = p * (1 - lr * wd)
+        mm = beta1 * mm + (1 - beta1) * g
+        vv = beta2 * vv + (1 - beta2) * g * g
+        mhat = mm / (1 - beta1 ** step)
+        vhat = vv / (1 - beta2 ** step)
+        p = p - lr * mhat / (vhat.sqrt() + eps)
+        out.append((p, mm, vv))
+    return out
+
+
+def linear_warmup_lambda(step, warmup, total):
+    """[HF] optimization.py:101-104 get_linear_schedule_with_warmup lr multiplier."""
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    return max(0.0, float(total - step) / float(max(1, total - warmup)))

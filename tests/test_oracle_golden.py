@@ -1,0 +1,131 @@
+"""Pin the CPU oracle (oracle/clip_ref.py) against goldens produced by running the
+reference itself (tools/gen_goldens.py).  CPU only."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from clipmi import config as C
+from clipmi import synth
+from oracle import clip_ref as R
+
+
+def digest(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()[:16]
+
+
+def model_params(cfg, adapters, requires_grad=False):
+    p = R.to_torch(synth.clip_state_dict(cfg, seed=0), requires_grad=requires_grad)
+    ta = va = None
+    if adapters:
+        ta = R.to_torch(synth.adapter_state_dict(cfg.text_config.hidden_size, 256, 0, "text_adapter"),
+                        requires_grad=requires_grad)
+        va = R.to_torch(synth.adapter_state_dict(cfg.vision_config.hidden_size, 256, 0, "vision_adapter"),
+                        requires_grad=requires_grad)
+    return p, ta, va
+
+
+def batch(cfg, B, g):
+    b = synth.synthetic_batch(cfg, B, seed=1234)
+    assert digest(b["pixel_values"], b["input_ids"], b["attention_mask"]) == str(g["input_digest"])
+    return {k: torch.from_numpy(v) for k, v in b.items()}
+
+
+@pytest.mark.parametrize("tag,preset,B,adapters", [
+    ("tiny", "tiny", 4, True),
+    ("b32", "B/32", 8, True),
+    ("b32_noadapter", "B/32", 8, False),
+    ("b16", "B/16", 4, False),
+])
+def test_forward_matches_reference(golden, tag, preset, B, adapters):
+    g = golden(f"forward_{tag}.npz")
+    cfg = C.resolve(preset)
+    p, ta, va = model_params(cfg, adapters)
+    with torch.no_grad():
+        out = R.clip_with_adapters_forward(batch(cfg, B, g), p, cfg, ta, va)
+    for k in ("logits_per_text", "text_features", "image_features"):
+        np.testing.assert_allclose(out[k].numpy(), g[k], atol=2e-5, rtol=1e-4, err_msg=k)
+    np.testing.assert_allclose(out["loss"].item(), g["loss"], atol=1e-5)
+    # Q1: first-token pooling makes every text row identical
+    t = out["text_features"].numpy()
+    assert np.allclose(t, t[:1], atol=1e-6)
+
+
+def test_eos_pooling_matches_hf(golden):
+    g = golden("forward_b32.npz")
+    cfg = C.resolve("B/32")
+    p, _, _ = model_params(cfg, False)
+    b = batch(cfg, 8, g)
+    with torch.no_grad():
+        tf = R.text_features(b["input_ids"], b["attention_mask"], p, cfg, None, pooling="eos")
+        h = R.text_tower(b["input_ids"], b["attention_mask"], p, cfg)
+    np.testing.assert_allclose(tf.numpy(), g["text_eos_projected"], atol=2e-5, rtol=1e-4)
+    np.testing.assert_allclose(h[:, :8].numpy(), g["text_last_hidden"], atol=2e-5, rtol=1e-4)
+
+
+def test_encoder_layer_matches_hf(golden):
+    g = golden("forward_b16.npz")
+    cfg = C.resolve("B/16")
+    v = cfg.vision_config
+    p, _, _ = model_params(cfg, False)
+    x = torch.from_numpy(synth.normal((2, v.num_positions, v.hidden_size), 3, "layer_x"))
+    assert digest(x.numpy()) == str(g["layer0_x_digest"])
+    with torch.no_grad():
+        y = R.encoder_layer(x, p, "vision_model.encoder.layers.0", v.num_attention_heads, v.layer_norm_eps, None)
+    np.testing.assert_allclose(y.numpy(), g["layer0_y"], atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag,D,ln", [("text", 512, True), ("vision", 768, True), ("textual", 512, False)])
+def test_adapters_fwd_bwd(golden, tag, D, ln):
+    g = golden("adapters.npz")
+    a = R.to_torch(synth.adapter_state_dict(D, 256, 7, f"{tag}_adapter", ln=ln), requires_grad=True)
+    x = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/x")).requires_grad_(True)
+    gy = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/gy"))
+    y = R.adapter(x, a, layer_norm_on=ln)
+    y.backward(gy)
+    np.testing.assert_allclose(y.detach().numpy(), g[f"{tag}_y"], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(x.grad.numpy(), g[f"{tag}_gx"], atol=1e-5, rtol=1e-5)
+    for k, t in a.items():
+        kk = k if ln else k.replace("down_project", "down_proj").replace("up_project", "up_proj")
+        np.testing.assert_allclose(t.grad.numpy(), g[f"{tag}_g/{kk}"], atol=1e-5, rtol=1e-4, err_msg=k)
+
+
+@pytest.mark.parametrize("B,E", [(8, 64), (256, 512)])
+def test_contrastive(golden, B, E):
+    g = golden("contrastive.npz")
+    t = torch.from_numpy(synth.normal((B, E), 11, f"ct/{B}")).requires_grad_(True)
+    i = torch.from_numpy(synth.normal((B, E), 11, f"ci/{B}")).requires_grad_(True)
+    s = torch.tensor(C.LN100, requires_grad=True)
+    out = R.contrastive(t, i, s)
+    out["loss"].backward()
+    np.testing.assert_allclose(out["loss"].item(), g[f"B{B}_loss"], atol=1e-5)
+    np.testing.assert_allclose(out["logits_per_text"].detach().numpy(), g[f"B{B}_logits_per_text"], atol=1e-4)
+    np.testing.assert_allclose(t.grad.numpy(), g[f"B{B}_gt"], atol=1e-6)
+    np.testing.assert_allclose(i.grad.numpy(), g[f"B{B}_gi"], atol=1e-6)
+    np.testing.assert_allclose(s.grad.item(), g[f"B{B}_gscale"], atol=1e-5)
+
+
+@pytest.mark.parametrize("tag,adapters", [("tiny_adapter_grads", True), ("tiny_full_grads", False)])
+def test_tiny_gradients(golden, tag, adapters):
+    g = golden(f"forward_{tag}.npz")
+    cfg = C.resolve("tiny")
+    p, ta, va = model_params(cfg, adapters, requires_grad=True)
+    out = R.clip_with_adapters_forward(batch(cfg, 4, g), p, cfg, ta, va)
+    out["loss"].backward()
+    np.testing.assert_allclose(out["loss"].item(), g["loss"], atol=1e-5)
+    names = [k[5:] for k in g.files if k.startswith("grad/")]
+    assert names
+    for n in names:
+        if n.startswith("clip."):
+            t = p[n[5:]]
+        elif n.startswith("text_adapter."):
+            t = ta[n[len("text_adapter."):]]
+        else:
+            t = va[n[len("vision_adapter."):]]
+        ref = g["grad/" + n]
+        scale = max(1e-3, float(np.abs(ref).max()))
+        np.testing.assert_allclose(t.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=n)

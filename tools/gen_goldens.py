@@ -1,0 +1,226 @@
+"""Generate tests/golden/*.npz by running the REFERENCE's own Python in this container.
+
+Runs only where /root/reference exists (the build container).  It imports the
+reference's ``model_m.CLIPWithAdapters``, ``adapter.clip_adapter`` / ``adapter.peclip``
+and ``trainer.CLIPAdapterTrainer`` (nothing from them is copied into the repo), builds
+HF ``CLIPModel`` objects locally from ``clipmi.config`` presets with weights from the
+deterministic generator ``clipmi.synth`` (no hub access), and records inputs' checksums
++ outputs (+ gradients) as small fp32 fixtures.
+
+    python tools/gen_goldens.py            # writes tests/golden/*.npz, *.json
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, os.path.join(REPO, "vlm-clip_amd"))
+sys.path.insert(0, REF)
+
+from clipmi import config as C  # noqa: E402
+from clipmi import synth  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def digest(*arrays) -> str:
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()[:16]
+
+
+def build_reference_model(cfg, use_text_adapter=True, use_vision_adapter=True, freeze_clip=True, seed=0):
+    """Reference CLIPWithAdapters (model_m.py:15-65) on a locally saved CLIPModel."""
+    from transformers import CLIPConfig, CLIPModel, CLIPProcessor
+    import model_m
+    hf_cfg = CLIPConfig(**cfg.to_hf_dict())
+    m = CLIPModel(hf_cfg)
+    sd = {k: torch.from_numpy(v.copy()) for k, v in synth.clip_state_dict(cfg, seed=seed).items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("position_ids" in k for k in missing), missing
+    d = tempfile.mkdtemp(prefix="clipref_")
+    m.save_pretrained(d)
+    CLIPProcessor.from_pretrained = staticmethod(lambda *a, **k: None)  # processor unused in forward
+    ref = model_m.CLIPWithAdapters(clip_model_name=d, use_text_adapter=use_text_adapter,
+                                   use_vision_adapter=use_vision_adapter, use_shared_adapters=False,
+                                   freeze_clip=freeze_clip)
+    t, v = cfg.text_config, cfg.vision_config
+    if use_text_adapter:
+        ref.text_adapter.load_state_dict({k: torch.from_numpy(x) for k, x in
+                                          synth.adapter_state_dict(t.hidden_size, 256, seed, "text_adapter").items()})
+    if use_vision_adapter:
+        ref.vision_adapter.load_state_dict({k: torch.from_numpy(x) for k, x in
+                                            synth.adapter_state_dict(v.hidden_size, 256, seed, "vision_adapter").items()})
+    ref.eval()
+    return ref
+
+
+def batch_tensors(cfg, B, seed=1234):
+    b = synth.synthetic_batch(cfg, B, seed=seed)
+    return b, {k: torch.from_numpy(v) for k, v in b.items()}
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: (np.asarray(v, dtype=np.float32) if np.asarray(v).dtype.kind == "f" else np.asarray(v))
+                                 for k, v in arrays.items()})
+    print("wrote", path, f"{os.path.getsize(path) / 1e3:.0f} kB")
+
+
+def gen_adapters():
+    from adapter.clip_adapter import TextAdapter, VisionAdapter
+    from adapter.peclip import TextualAdapter
+    out = {}
+    for tag, cls, D in (("text", TextAdapter, 512), ("vision", VisionAdapter, 768), ("textual", TextualAdapter, 512)):
+        mod = cls(D, 256)
+        sd = synth.adapter_state_dict(D, 256, 7, f"{tag}_adapter", ln=(tag != "textual"))
+        if tag == "textual":
+            sd = {k.replace("down_project", "down_proj").replace("up_project", "up_proj"): v for k, v in sd.items()}
+        mod.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        x = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/x")).requires_grad_(True)
+        gy = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/gy"))
+        y = mod(x)
+        y.backward(gy)
+        out[f"{tag}_y"] = y.detach().numpy()
+        out[f"{tag}_gx"] = x.grad.numpy()
+        for k, p in mod.named_parameters():
+            out[f"{tag}_g/{k}"] = p.grad.numpy()
+    save("adapters.npz", **out)
+
+
+def gen_forward(preset, B, tag, adapters=True, grads=False, layer=False, freeze_clip=True):
+    cfg = C.resolve(preset)
+    ref = build_reference_model(cfg, adapters, adapters, freeze_clip=freeze_clip)
+    b_np, b = batch_tensors(cfg, B)
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"]))}
+    if grads:
+        ref.train()  # no dropout anywhere on the path (adapters have none, attention_dropout=0)
+        res = ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=b["pixel_values"])
+        res["loss"].backward()
+        for k, p in ref.named_parameters():
+            if p.grad is not None:
+                out[f"grad/{k}"] = p.grad.numpy()
+    else:
+        with torch.no_grad():
+            res = ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=b["pixel_values"])
+    for k, v in res.items():
+        out[k] = v.detach().numpy()
+    with torch.no_grad():
+        out["text_features_raw"] = ref.get_text_features(b["input_ids"], b["attention_mask"]).numpy()
+        out["image_features_raw"] = ref.get_image_features(b["pixel_values"]).numpy()
+        # HF pooler (EOS pooling) path for the optional pooling="eos" mode
+        to = ref.clip.text_model(input_ids=b["input_ids"], attention_mask=b["attention_mask"])
+        out["text_last_hidden"] = to.last_hidden_state.numpy()[:, :8]
+        out["text_eos_projected"] = ref.clip.text_projection(to.pooler_output).numpy()
+        vo = ref.clip.vision_model(pixel_values=b["pixel_values"])
+        out["vision_last_hidden_cls"] = vo.last_hidden_state.numpy()[:, 0]
+        if layer:
+            lay = ref.clip.vision_model.encoder.layers[0]
+            x = torch.from_numpy(synth.normal((2, cfg.vision_config.num_positions, cfg.vision_config.hidden_size),
+                                              3, "layer_x"))
+            out["layer0_x_digest"] = np.array(digest(x.numpy()))
+            out["layer0_y"] = lay(x, None).numpy()
+    save(f"forward_{tag}.npz", **out)
+
+
+def gen_contrastive():
+    """The contrastive branch alone (model_m.py:146-171), fed synthetic features."""
+    cfg = C.resolve("tiny")
+    ref = build_reference_model(cfg, False, False)
+    out = {}
+    for B, E in ((8, 64), (256, 512)):
+        t = torch.from_numpy(synth.normal((B, E), 11, f"ct/{B}")).requires_grad_(True)
+        i = torch.from_numpy(synth.normal((B, E), 11, f"ci/{B}")).requires_grad_(True)
+        ref.get_text_features = lambda *a, **k: t
+        ref.get_image_features = lambda *a, **k: i
+        ref.clip.logit_scale.requires_grad_(True)
+        ref.clip.logit_scale.grad = None
+        res = ref(input_ids=torch.zeros(B, 1, dtype=torch.long), attention_mask=torch.ones(B, 1),
+                  pixel_values=torch.zeros(B, 1))
+        res["loss"].backward()
+        out[f"B{B}_loss"] = res["loss"].detach().numpy()
+        out[f"B{B}_logits_per_text"] = res["logits_per_text"].detach().numpy()
+        out[f"B{B}_gt"] = t.grad.numpy()
+        out[f"B{B}_gi"] = i.grad.numpy()
+        out[f"B{B}_gscale"] = ref.clip.logit_scale.grad.numpy()
+    save("contrastive.npz", **out)
+
+
+def gen_trainer():
+    """Three optimizer steps of the reference CLIPAdapterTrainer (trainer.py:16-124)."""
+    from torch.utils.data import DataLoader, Dataset
+    import trainer as ref_trainer
+    cfg = C.resolve("tiny")
+    ref = build_reference_model(cfg, True, True)
+    b_np = synth.synthetic_batch(cfg, 12, seed=99)
+
+    class Fixed(Dataset):
+        def __len__(self):
+            return 12
+
+        def __getitem__(self, i):
+            return {k: torch.from_numpy(v[i]) for k, v in b_np.items()}
+
+    dl = DataLoader(Fixed(), batch_size=4, shuffle=False)
+    tmp = tempfile.mkdtemp(prefix="clipref_tr_")
+    tr = ref_trainer.CLIPAdapterTrainer(ref, dl, learning_rate=1e-3, weight_decay=0.01, warmup_steps=1,
+                                        max_grad_norm=1.0, output_dir=tmp)
+    tr.train(num_epochs=1, save_every=1)
+    out = {f"param/{k}": p.detach().numpy() for k, p in ref.named_parameters() if "adapter" in k}
+    out["input_digest"] = np.array(digest(*b_np.values()))
+    save("trainer_tiny.npz", **out)
+
+
+def gen_checkpoint_schema():
+    """Key/shape schema of the reference's checkpoint fixture (safe loader only)."""
+    sd = torch.load(os.path.join(REF, "test_checkpoints", "test_adapter.pt"), map_location="cpu", weights_only=True)
+    schema = {top: {k: list(v.shape) for k, v in sub.items()} for top, sub in sd.items()}
+    with open(os.path.join(OUT, "test_adapter_schema.json"), "w") as f:
+        json.dump(schema, f, indent=1, sort_keys=True)
+    print("schema", schema)
+
+
+def gen_quirks():
+    cfg = C.resolve("tiny")
+    from transformers import CLIPConfig, CLIPModel, CLIPProcessor
+    import model_m
+    hf = CLIPModel(CLIPConfig(**cfg.to_hf_dict()))
+    d = tempfile.mkdtemp(prefix="clipref_q_")
+    hf.save_pretrained(d)
+    CLIPProcessor.from_pretrained = staticmethod(lambda *a, **k: None)
+    ref = model_m.CLIPWithAdapters(clip_model_name=d, use_shared_adapters=True)
+    _, b = batch_tensors(cfg, 4)
+    err = ""
+    try:
+        ref(**b)
+    except Exception as e:  # Q3: shared adapters crash for B>1
+        err = type(e).__name__
+    with open(os.path.join(OUT, "quirks.json"), "w") as f:
+        json.dump({"shared_adapters_B4_error": err}, f)
+    print("Q3 error:", err)
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    gen_checkpoint_schema()
+    gen_quirks()
+    gen_adapters()
+    gen_contrastive()
+    gen_forward("tiny", 4, "tiny", adapters=True, grads=False)
+    gen_forward("tiny", 4, "tiny_adapter_grads", adapters=True, grads=True)
+    gen_forward("tiny", 4, "tiny_full_grads", adapters=False, grads=True, freeze_clip=False)
+    gen_trainer()
+    gen_forward("B/32", 8, "b32", adapters=True, layer=False)
+    gen_forward("B/32", 8, "b32_noadapter", adapters=False)
+    gen_forward("B/16", 4, "b16", adapters=False, layer=True)
