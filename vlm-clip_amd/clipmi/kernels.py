@@ -1,0 +1,84 @@
+"""Thin tensor-level wrappers over the libclipmi C ABI.
+
+Every function enqueues on torch's current HIP stream and never synchronises.  Shapes
+are validated here and again in C; tensors must live on the GPU (the product path has
+no CPU fallback)."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, GemmDesc
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise ValueError(f"unsupported dtype {t.dtype}") from None
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _on_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("libclipmi ops need GPU tensors (no CPU fallback)")
+
+
+def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, residual=None, ldr=0,
+         aux=None, ldaux=0, alpha=1.0, flags=0, split_k=1, workspace=None):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see include/clipmi.h clipmi_gemm."""
+    _on_gpu(A, B, C, bias, residual, aux, workspace)
+    if A.dtype != B.dtype:
+        raise ValueError("A and B must share a dtype")
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = A.data_ptr(), lda, int(a_kmajor)
+    d.B, d.ldb, d.b_kmajor = B.data_ptr(), ldb, int(b_kmajor)
+    d.C, d.ldc = C.data_ptr(), ldc
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.residual, d.ldr = (residual.data_ptr() if residual is not None else None), ldr
+    d.aux, d.ldaux = (aux.data_ptr() if aux is not None else None), ldaux
+    d.alpha, d.flags = alpha, flags
+    d.ab_dtype, d.c_dtype = dt(A), dt(C)
+    d.bias_dtype = dt(bias) if bias is not None else F32
+    d.split_k = split_k
+    if workspace is not None:
+        d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    _lib.check(_lib.lib().clipmi_gemm(stream(), ctypes.byref(d)), "clipmi_gemm")
+    return C
+
+
+def linear(x, w, bias=None, *, act=None, residual=None, out=None, pre_out=None):
+    """y = act(x @ w.T + bias) (+ residual): nn.Linear forward on the MFMA GEMM."""
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    flags = 0
+    if bias is not None:
+        flags |= _lib.EPI_BIAS
+    if act == "quick_gelu":
+        flags |= _lib.EPI_QGELU
+    elif act == "gelu":
+        flags |= _lib.EPI_GELU
+    if residual is not None:
+        flags |= _lib.EPI_RESID
+    if pre_out is not None:
+        flags |= _lib.EPI_STORE_PRE
+    gemm(M, N, K, x2, x2.stride(0), True, w, w.stride(0), True, out, out.stride(0), bias=bias,
+         residual=residual.reshape(-1, N) if residual is not None else None, ldr=N,
+         aux=pre_out, ldaux=N, flags=flags)
+    return out.view(*x.shape[:-1], N)

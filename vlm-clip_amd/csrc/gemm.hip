@@ -1,0 +1,400 @@
+// MFMA GEMM for gfx950 with fused epilogues.
+//
+// Replaces every nn.Linear on the hot path (forward, dgrad and wgrad):
+//   [HF] modeling_clip.py:313-315,332 (q/k/v/out_proj), :348-350 (fc1/fc2),
+//   adapter/clip_adapter.py:19-21,146-148 (adapter down/up), model_m.py:103,123 (projections).
+//
+// Design (bf16 path):
+//   * 128x128 output tile per 256-thread workgroup, 4 waves in 2x2, each wave 64x64 =
+//     4x4 tiles of v_mfma_f32_16x16x32_bf16, fp32 accumulators (64 VGPRs).
+//   * K step 64, register-staged global->LDS copy (16 B per lane), two LDS buffers,
+//     one barrier per K step; the next tile's global loads are in flight while the
+//     current tile's MFMAs run.
+//   * Either operand may be k-major ([rows][K], the forward's x and W) or row-major in
+//     k ([K][rows], the dgrad's W and both wgrad operands).  k-major tiles are read with
+//     ds_read_b128, the other layout with ds_read_b64_tr_b16 (hardware transpose), so
+//     backward GEMMs need no transpose pass over HBM.
+//   * LDS images are XOR-swizzled (checked conflict-free for the reads and the
+//     b128 writes against the gfx950 bank rules, tools/lds_banks.py).
+//   * Operands are swapped in the MFMA (acc = W-tile x X-tile) so each lane ends with 4
+//     consecutive output columns: 8-byte bf16 / 16-byte fp32 epilogue stores.
+//   * Epilogue fuses bias, quick_gelu / gelu_erf (and their derivatives for dgrad),
+//     residual add, accumulate-into-C and pre-activation store.
+//   * blockIdx is remapped XCD-aware so neighbouring tiles share an XCD's L2.
+//   * split-K (wgrad, K = tokens) writes fp32 partial slabs, summed by a reduce kernel.
+// f32 path: exact-f32 LDS-tiled SIMT kernel with the same epilogue (parity mode).
+#include "common.h"
+#include "internal.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+
+struct GemmP {
+  int M, N, K;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  const void* bias; const void* res; int64_t ldr;
+  void* aux; int64_t ldaux;
+  float alpha; int flags; int bias_f32;
+  int k_per_split; float* ws;
+  int tiles_n, ntiles;
+};
+
+__device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
+  return p.bias_f32 ? ((const float*)p.bias)[n] : (float)((const bf16*)p.bias)[n];
+}
+
+// v holds C[m][n..n+3] before the epilogue.
+template <typename OutT>
+__device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[4]) {
+  const int f = p.flags;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] *= p.alpha;
+  if (f & CLIPMI_EPI_BIAS) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += ld_bias(p, n + j);
+  }
+  if (f & CLIPMI_EPI_STORE_PRE) store4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v);
+  if (f & CLIPMI_EPI_QGELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
+  } else if (f & CLIPMI_EPI_GELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+  }
+  if (f & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)) {
+    float a[4];
+    load4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, a);
+    if (f & CLIPMI_EPI_DQGELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= quick_gelu_grad(a[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= gelu_erf_grad(a[j]);
+    }
+  }
+  if (f & CLIPMI_EPI_RESID) {
+    float r[4];
+    load4((const OutT*)p.res + (int64_t)m * p.ldr + n, r);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += r[j];
+  }
+  OutT* c = (OutT*)p.C + (int64_t)m * p.ldc + n;
+  if (f & CLIPMI_EPI_BETA) {
+    float o[4];
+    load4(c, o);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += o[j];
+  }
+  store4(c, v);
+}
+
+// ---------------------------------------------------------------- LDS images
+// k-major image: [128 rows][64 k] bf16, 128-B rows, 16-B chunk c stored at c ^ ((r>>1)&7)
+__device__ __forceinline__ int kimg_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+// row-major-in-k image: [64 k][128 rows] bf16, 256-B rows, chunk c stored at c ^ 2*g(r)
+__device__ __forceinline__ int mimg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+__device__ __forceinline__ int mimg_off(int r, int c) { return r * 256 + ((c ^ mimg_swz(r)) << 4); }
+
+// Global -> register staging of one 128x64 operand tile (4 x 16 B per thread).
+template <bool KMAJ>
+struct Stager {
+  const bf16* base[4];  // per pass: k-major -> row start (+chunk), else column chunk start
+  int lds_off[4];
+  int chunk_k[4];       // k-major: element offset of the chunk within the K step; else k row
+  __device__ __forceinline__ void init(const bf16* X, int64_t ld, int row0, int R, int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int id = i * NTHR + t;
+      if (KMAJ) {
+        int r = id >> 3, c = id & 7;
+        int gr = min(row0 + r, R - 1);
+        base[i] = X + (int64_t)gr * ld + c * 8;
+        chunk_k[i] = c * 8;
+        lds_off[i] = kimg_off(r, c);
+      } else {
+        int kr = id >> 4, c = id & 15;
+        int gc = min(row0 + c * 8, R - 8);
+        base[i] = X + (int64_t)kr * ld + gc;
+        chunk_k[i] = kr;
+        lds_off[i] = mimg_off(kr, c);
+      }
+    }
+  }
+  __device__ __forceinline__ void load(u32x4 v[4], int k0, int64_t ld, int kvalid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16* g = KMAJ ? base[i] + k0 : base[i] + (int64_t)k0 * ld;
+      if (kvalid >= BK || chunk_k[i] < kvalid) v[i] = *(const u32x4*)g;
+      else v[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, const u32x4 v[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *LDS_PTR(u32x4, lds + lds_off[i]) = v[i];
+  }
+};
+
+// One 16x32 MFMA operand fragment: rows rb..rb+15 of the tile, k = kk*32 .. kk*32+31.
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int kk, int lane) {
+  if (KMAJ) {
+    int r = rb + (lane & 15), c = kk * 4 + (lane >> 4);
+    return *LDS_PTR(const bf16x8, lds + kimg_off(r, c));
+  } else {
+    int q = (lane & 15) >> 2, p4 = lane & 3;
+    int m = rb + 4 * p4;
+    int r0 = kk * 32 + 8 * (lane >> 4) + q;
+    int r1 = r0 + 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(s16x4, lds + mimg_off(r0, m >> 3) + (m & 7) * 2));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(s16x4, lds + mimg_off(r1, m >> 3) + (m & 7) * 2));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+template <bool AK, bool BKM, typename OutT>
+__global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tile = xcd_remap(blockIdx.x, p.ntiles);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  Stager<AK> sa;
+  Stager<BKM> sb;
+  sa.init((const bf16*)p.A, p.lda, m0, p.M, t);
+  sb.init((const bf16*)p.B, p.ldb, n0, p.N, t);
+
+  // LDS: [buf][A 16KB | B 16KB]
+#define LDSA(b) (smem + (b) * 32768)
+#define LDSB(b) (smem + (b) * 32768 + 16384)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  if (nk > 0) {
+    sa.load(ra, kbeg, p.lda, kend - kbeg);
+    sb.load(rb, kbeg, p.ldb, kend - kbeg);
+    sa.store(LDSA(0), ra);
+    sb.store(LDSB(0), rb);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < nk;
+    if (more) {
+      const int k1 = kbeg + (it + 1) * BK;
+      sa.load(ra, k1, p.lda, kend - k1);
+      sb.load(rb, k1, p.ldb, kend - k1);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<AK>(LDSA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<BKM>(LDSB(cur), wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(LDSA(cur ^ 1), ra);
+      sb.store(LDSB(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+
+#undef LDSA
+#undef LDSB
+  // acc[i][j][r] = C[m0 + wm*64 + i*16 + (lane&15)][n0 + wn*64 + j*16 + (lane>>4)*4 + r]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.ws) {
+        store4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v);
+      } else {
+        epilogue4<OutT>(p, m, n, v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ f32 SIMT path
+constexpr int FT = 64, FK = 16;
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p, int akm, int bkm) {
+  __shared__ float As[FK][FT + 4];
+  __shared__ float Bs[FK][FT + 4];
+  const float* A = (const float*)p.A;
+  const float* B = (const float*)p.B;
+  const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  const int tile = blockIdx.x;
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * FT, n0 = tn * FT;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  float acc[4][4] = {};
+  for (int k0 = kbeg; k0 < kend; k0 += FK) {
+    for (int e = t; e < FK * FT; e += 256) {
+      int kk, r;
+      if (akm) { r = e / FK; kk = e % FK; } else { kk = e / FT; r = e % FT; }
+      int gm = m0 + r, gk = k0 + kk;
+      float va = 0.f;
+      if (gm < p.M && gk < kend) va = akm ? A[(int64_t)gm * p.lda + gk] : A[(int64_t)gk * p.lda + gm];
+      As[kk][r] = va;
+      if (bkm) { r = e / FK; kk = e % FK; } else { kk = e / FT; r = e % FT; }
+      int gn = n0 + r;
+      gk = k0 + kk;
+      float vb = 0.f;
+      if (gn < p.N && gk < kend) vb = bkm ? B[(int64_t)gn * p.ldb + gk] : B[(int64_t)gk * p.ldb + gn];
+      Bs[kk][r] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < FK; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + ty * 4 + i, n = n0 + tx * 4;
+    if (m >= p.M || n >= p.N) continue;
+    float v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+    if (p.ws) store4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v);
+    else epilogue4<OutT>(p, m, n, v);
+  }
+}
+
+// split-K reduction: C (fp32) = [C +] alpha * sum_z ws[z]
+__global__ void splitk_reduce_kernel(const float* ws, float* C, int64_t ldc, int M, int N, int splits,
+                                     float alpha, int beta) {
+  int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  int64_t total = (int64_t)M * N;
+  if (i4 >= total) return;
+  int m = (int)(i4 / N), n = (int)(i4 - (int64_t)m * N);
+  f32x4 s = *(const f32x4*)(ws + i4);
+  for (int z = 1; z < splits; ++z) s += *(const f32x4*)(ws + (int64_t)z * total + i4);
+  float* c = C + (int64_t)m * ldc + n;
+  f32x4 o = s * alpha;
+  if (beta) o += *(const f32x4*)c;
+  *(f32x4*)c = o;
+}
+
+template <bool AK, bool BKM, typename OutT>
+void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
+}
+
+}  // namespace
+
+extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
+  if (d->M == 0 || d->N == 0) return CLIPMI_OK;
+  CLIPMI_REQUIRE(d->N % 8 == 0, "N must be a multiple of 8");
+  CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32 || d->c_dtype == CLIPMI_BF16, "c_dtype");
+  const bool bf = d->ab_dtype == CLIPMI_BF16;
+  CLIPMI_REQUIRE(bf || d->ab_dtype == CLIPMI_F32, "ab_dtype");
+  if (bf) {
+    CLIPMI_REQUIRE(!d->a_kmajor || d->K % 8 == 0, "k-major A needs K % 8 == 0");
+    CLIPMI_REQUIRE(!d->b_kmajor || d->K % 8 == 0, "k-major B needs K % 8 == 0");
+    CLIPMI_REQUIRE(d->a_kmajor || d->M % 8 == 0, "row-major A needs M % 8 == 0");
+    CLIPMI_REQUIRE(d->a_kmajor || d->M >= 8, "M >= 8");
+    CLIPMI_REQUIRE(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0, "A/B must be 16-byte aligned");
+    CLIPMI_REQUIRE((d->lda % 8) == 0 && (d->ldb % 8) == 0, "lda/ldb must be multiples of 8");
+  }
+  CLIPMI_REQUIRE((d->ldc % 4) == 0, "ldc must be a multiple of 4");
+  int splits = d->split_k > 1 ? d->split_k : 1;
+  GemmP p;
+  p.M = d->M; p.N = d->N; p.K = d->K;
+  p.A = d->A; p.lda = d->lda; p.B = d->B; p.ldb = d->ldb;
+  p.C = d->C; p.ldc = d->ldc; p.bias = d->bias; p.res = d->residual; p.ldr = d->ldr;
+  p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
+  p.bias_f32 = d->bias_dtype == CLIPMI_F32;
+  p.ws = nullptr;
+  const int tile = bf ? BM : FT;
+  const int kstep = bf ? BK : FK;
+  if (splits > 1) {
+    CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32, "split_k needs fp32 C");
+    CLIPMI_REQUIRE((d->flags & ~CLIPMI_EPI_BETA) == 0, "split_k supports only the beta flag");
+    CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4, "split_k workspace too small");
+    int per = (d->K + splits - 1) / splits;
+    per = (per + kstep - 1) / kstep * kstep;
+    splits = (d->K + per - 1) / per;
+    p.k_per_split = per;
+    p.ws = (float*)d->workspace;
+  } else {
+    p.k_per_split = d->K > 0 ? d->K : 1;
+  }
+  p.tiles_n = (d->N + tile - 1) / tile;
+  p.ntiles = p.tiles_n * ((d->M + tile - 1) / tile);
+  if (bf) {
+    const bool f32o = d->c_dtype == CLIPMI_F32 || p.ws;
+    const int sel = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
+    if (f32o) {
+      switch (sel) {
+        case 3: launch_bf16<true, true, float>(p, splits, s); break;
+        case 2: launch_bf16<true, false, float>(p, splits, s); break;
+        case 1: launch_bf16<false, true, float>(p, splits, s); break;
+        default: launch_bf16<false, false, float>(p, splits, s); break;
+      }
+    } else {
+      switch (sel) {
+        case 3: launch_bf16<true, true, bf16>(p, splits, s); break;
+        case 2: launch_bf16<true, false, bf16>(p, splits, s); break;
+        case 1: launch_bf16<false, true, bf16>(p, splits, s); break;
+        default: launch_bf16<false, false, bf16>(p, splits, s); break;
+      }
+    }
+  } else {
+    if (d->c_dtype == CLIPMI_F32 || p.ws)
+      hipLaunchKernelGGL(gemm_f32_kernel<float>, dim3(p.ntiles, splits), dim3(256), 0, s, p, d->a_kmajor, d->b_kmajor);
+    else
+      hipLaunchKernelGGL(gemm_f32_kernel<bf16>, dim3(p.ntiles, splits), dim3(256), 0, s, p, d->a_kmajor, d->b_kmajor);
+  }
+  CLIPMI_CHECK_LAUNCH();
+  if (p.ws) {
+    int64_t total4 = ((int64_t)d->M * d->N) / 4;
+    CLIPMI_REQUIRE(((int64_t)d->M * d->N) % 4 == 0, "M*N % 4");
+    CLIPMI_REQUIRE(d->ldc == d->N || d->M == 1 || true, "");
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s,
+                       p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha,
+                       (d->flags & CLIPMI_EPI_BETA) ? 1 : 0);
+    CLIPMI_CHECK_LAUNCH();
+  }
+  return CLIPMI_OK;
+}

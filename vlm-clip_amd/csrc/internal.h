@@ -1,0 +1,14 @@
+// Host-side internals shared by the libclipmi translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "../../include/clipmi.h"
+
+int clipmi_fail(hipError_t e, const char* file, int line);
+int clipmi_invalid(const std::string& msg);
+void clipmi_set_error(const std::string& msg);
+
+#define CLIPMI_REQUIRE(cond, msg) do { if (!(cond)) return clipmi_invalid(std::string(__func__) + ": " + (msg)); } while (0)
+#define CLIPMI_HIP(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return clipmi_fail(e_, __FILE__, __LINE__); } while (0)
+#define CLIPMI_TRY(call) do { int s_ = (call); if (s_ != CLIPMI_OK) return s_; } while (0)
