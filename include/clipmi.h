@@ -66,6 +66,106 @@ typedef struct clipmi_gemm_desc {
 
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
 
+/* ---- LayerNorm ([HF] modeling_clip.py:357,359,605,642,559; adapter/clip_adapter.py:15,142) -------
+ * y = LN(x [+ pos[row % period] (+ cls at row % period == 0)]) * w + b; mean/rstd saved (fp32).
+ * With pos != NULL the sum is written back to x: the vision embedding ([HF] :209-219) fused
+ * into pre_layrnorm. Weights in the activation dtype. D % 64 == 0, D <= 1024. */
+int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy, const void* w,
+                         const void* b, float* mean, float* rstd, int R, int D, float eps, const void* pos,
+                         const void* cls, int period);
+int64_t clipmi_layernorm_bwd_ws(int R, int D);
+/* dx = [dres +] LN'(dy); dw/db (fp32, may be NULL) accumulate when beta_wb. */
+int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                         const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
+                         int64_t ldres, float* dw, float* db, int beta_wb, void* ws, int64_t ws_bytes, int R, int D);
+/* out[n] (+)= sum_r x[r][n]  (bias gradients of every Linear on the path) */
+int64_t clipmi_colsum_ws(int R, int N);
+int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, int N, float* out, int beta, void* ws,
+                  int64_t ws_bytes);
+/* out[t][c] (+)= sum_b x[(b*period+t)][c] for t < nt  (position / class embedding gradients) */
+int clipmi_period_sum(void* stream, int dtype, const void* x, int64_t ldx, int nb, int period, int nt, int D,
+                      float* out, int beta);
+
+/* ---- Embeddings ------------------------------------------------------------------------------
+ * text: x0[r] = tok[ids[r]] + pos[r % S]   ([HF] CLIPTextEmbeddings.forward :232-256);
+ * *bad_flag |= 1 on an out-of-vocabulary id (Python raises IndexError like nn.Embedding). */
+int clipmi_text_embed(void* stream, int dtype, const int64_t* ids, const void* tok, const void* pos, void* x0, int R,
+                      int S, int D, int V, int* bad_flag);
+int64_t clipmi_text_embed_bwd_ws(int R, int V);
+/* gtok[v] (+)= sum_{r: ids[r]==v} dx0[r]  (counting sort, one wave per id, no float atomics) */
+int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids, const void* dx0, int R, int D, int V,
+                          float* gtok, int beta, void* ws, int64_t ws_bytes);
+/* vision: Conv2d(k=s=P, no bias) as im2col + GEMM ([HF] :148-154, :211-212).  X is
+ * [B*(G*G+1), Kp] with a zero row in each image's CLS slot, K index c*P*P+ky*P+kx. */
+int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, int C, int H, int P, int Kp);
+/* pooled token per row: mode 0 first token (model_m.py:102), 1 first EOS, 2 argmax id ([HF] :561-581) */
+int clipmi_pool_index(void* stream, const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx);
+int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* out);
+int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* dst,
+                        int beta);
+
+/* ---- Attention (head_dim 64, N <= 256) ([HF] CLIPAttention :298-335, eager core :259-277) -----
+ * qkv: [B*N, 3D] (q | k | v, head h at h*64), o: [B*N, D], lse: [B*H*N] fp32.
+ * attention_mask: int64 [B, N] key padding (1 keep) or NULL; causal for the text tower. */
+int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse, const int64_t* attention_mask,
+                         int causal, int B, int H, int N, int D);
+int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, const void* o, const float* lse, const void* dout,
+                         void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
+
+/* ---- Encoder engine: whole CLIPEncoder fwd/bwd in one call ([HF] :477-482, :362-383) ---------- */
+typedef struct clipmi_layer_w { /* activation dtype; qkv_w = [q;k;v] rows, [3D, D] */
+  const void *ln1_w, *ln1_b, *qkv_w, *qkv_b, *out_w, *out_b, *ln2_w, *ln2_b, *fc1_w, *fc1_b, *fc2_w, *fc2_b;
+} clipmi_layer_w;
+typedef struct clipmi_layer_grad { /* fp32, accumulated */
+  float *ln1_w, *ln1_b, *qkv_w, *qkv_b, *out_w, *out_b, *ln2_w, *ln2_b, *fc1_w, *fc1_b, *fc2_w, *fc2_b;
+} clipmi_layer_grad;
+typedef struct clipmi_layer_act { /* saved activations; pre == NULL in inference */
+  void *x_in, *ln1, *qkv, *o, *h, *ln2, *pre, *act;
+  float *mean1, *rstd1, *lse, *mean2, *rstd2;
+} clipmi_layer_act;
+typedef struct clipmi_encoder_desc {
+  int dtype, B, N, D, F, H, L;
+  float eps;
+  int causal;
+  const int64_t* attention_mask;
+  const clipmi_layer_w* layers;  /* [L] */
+  clipmi_layer_grad* grads;      /* [L], backward only */
+  clipmi_layer_act* act;         /* [L]; layer l writes its output to act[l+1].x_in (x_out for the last) */
+  void* x_out;
+  void* workspace;
+  int64_t workspace_bytes;
+} clipmi_encoder_desc;
+int clipmi_encoder_fwd(void* stream, const clipmi_encoder_desc* d);
+int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d);
+/* dx: dL/d(encoder output) in, dL/d(encoder input) out */
+int clipmi_encoder_bwd(void* stream, const clipmi_encoder_desc* d, void* dx);
+
+/* ---- Contrastive head (model_m.py:146-171), fp32 -------------------------------------------- */
+int clipmi_l2norm_fwd(void* stream, const float* x, float* y, float* nrm, int B, int E);
+int clipmi_l2norm_bwd(void* stream, const float* dy, const float* y, const float* nrm, float* dx, int B, int E);
+/* logits = exp(*logit_scale) * S over a [B, Bg] cosine block; lse, ce per row (label0 + i) */
+int clipmi_contrastive_ce_fwd(void* stream, const float* S, float* logits, const float* logit_scale, int B, int Bg,
+                              int label0, float* lse, float* ce);
+/* dS = g*exp(ls)*(softmax - onehot)*norm ; dls_row = sum_j dlogit*logit */
+int clipmi_contrastive_ce_bwd(void* stream, const float* logits, const float* lse, const float* logit_scale,
+                              const float* grad_out, int B, int Bg, int label0, float norm, float* dS, float* dls_row);
+int clipmi_sum2(void* stream, const float* a, const float* b, int n, float scale, float* out, int beta);
+
+/* ---- Optimizer (trainer.py:95,98; [HF] optimization.py:101-129) ------------------------------ */
+int64_t clipmi_grad_norm_ws(void);
+/* norm_out[0] = ||g||_2, norm_out[1] = min(1, max_norm/(norm+1e-6)) (device memory) */
+int clipmi_grad_norm(void* stream, const float* g, int64_t n, float max_norm, float* norm_out, void* ws,
+                     int64_t ws_bytes);
+int64_t clipmi_grad_norm_multi_ws(int count);
+int clipmi_grad_norm_multi(void* stream, const float* const* gs, const int64_t* ns, int count, float max_norm,
+                           float* norm_out, void* ws, int64_t ws_bytes);
+int clipmi_grad_scale(void* stream, float* g, int64_t n, const float* norm_out);
+/* torch.optim.AdamW step on a flat fp32 arena; grads scaled by clip[1] when clip != NULL;
+ * shadow (bf16, may be NULL) refreshed from the new parameters. */
+int clipmi_adamw(void* stream, float* p, const float* g, float* m, float* v, void* shadow_bf16, int64_t n, double lr,
+                 double beta1, double beta2, double eps, double weight_decay, int step, const float* clip);
+int clipmi_cast_f32_bf16(void* stream, const float* src, void* dst, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,210 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every entry
+point include/clipmi.h declares; parameter names/shapes match HF CLIPModel and the
+reference adapter checkpoint; the trainer's error behaviour; the data-parallel
+contrastive decomposition over a 2-rank gloo group."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from clipmi import config as C
+from clipmi import synth
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "clipmi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(clipmi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from clipmi import _lib
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.clipmi_version() >= 1
+
+
+def test_invalid_args_raise_without_gpu():
+    """Argument validation runs on the host before any launch."""
+    from clipmi import _lib
+    from clipmi._lib import GemmDesc
+    import ctypes
+    d = GemmDesc()
+    d.M, d.N, d.K = 16, 12, 64  # N % 8 != 0
+    d.ab_dtype = d.c_dtype = 1
+    st = _lib.lib().clipmi_gemm(None, ctypes.byref(d))
+    assert st == -1 and b"multiple of 8" in _lib.lib().clipmi_last_error()
+    with pytest.raises(ValueError):
+        _lib.check(st, "clipmi_gemm")
+
+
+def test_param_names_match_hf_clipmodel():
+    from transformers import CLIPConfig, CLIPModel
+    from clipmi.modules import CLIPParams
+    cfg = C.resolve("tiny")
+    hf = CLIPModel(CLIPConfig(**cfg.to_hf_dict()))
+    ours = CLIPParams(cfg, "cpu", shadow=False)
+    hs = {k: tuple(v.shape) for k, v in hf.state_dict().items() if not k.endswith("position_ids")}
+    os_ = {k: tuple(v.shape) for k, v in ours.state_dict().items()}
+    assert hs == os_
+    # HF state dict loads into the arena-backed module and round-trips
+    ours.load_state_dict(hf.state_dict(), strict=False)
+    for k, v in hf.state_dict().items():
+        if k in os_:
+            assert torch.equal(ours.state_dict()[k], v)
+
+
+def test_adapter_checkpoint_schema_matches_reference_fixture(golden):
+    from clipmi.modules import AdapterParams
+    schema = json.load(open(os.path.join(REPO, "tests", "golden", "test_adapter_schema.json")))
+    for key, hidden in (("text_adapter", 512), ("vision_adapter", 768)):
+        a = AdapterParams(hidden, 256, "cpu", shadow=False)
+        assert {k: list(v.shape) for k, v in a.state_dict().items()} == schema[key]
+
+
+def test_model_construction_and_checkpoint_roundtrip_cpu(tmp_path):
+    from clipmi import CLIPWithAdapters
+    m = CLIPWithAdapters("tiny", use_shared_adapters=False, device="cpu")
+    assert all(not p.requires_grad for p in m.clip.parameters())
+    assert all(p.requires_grad for n, p in m.named_parameters() if "adapter" in n)
+    assert abs(m.clip.logit_scale.item() - C.LN100) < 1e-6
+    path = str(tmp_path / "sub" / "ad.pt")
+    m.save_adapter_weights(path)
+    m2 = CLIPWithAdapters("tiny", use_shared_adapters=False, device="cpu", init_seed=5)
+    assert not torch.equal(m2.text_adapter.down_project.weight, m.text_adapter.down_project.weight)
+    m2.load_adapter_weights(path)
+    assert torch.equal(m2.text_adapter.down_project.weight, m.text_adapter.down_project.weight)
+    sd = torch.load(path, weights_only=True)
+    assert set(sd) == {"text_adapter", "vision_adapter"}
+    m3 = CLIPWithAdapters("tiny", use_vision_adapter=False, use_shared_adapters=False, device="cpu")
+    with pytest.raises(ValueError, match="Vision adapter weights found"):
+        m3.load_adapter_weights(path)
+    with pytest.raises(FileNotFoundError):
+        m3.load_adapter_weights(str(tmp_path / "nope.pt"))
+    m4 = CLIPWithAdapters("tiny", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                          device="cpu")
+    with pytest.raises(ValueError, match="No adapters enabled"):
+        m4.save_adapter_weights(path)
+
+
+def test_trainer_empty_param_list_raises_like_torch():
+    from clipmi import CLIPWithAdapters, CLIPAdapterTrainer
+    m = CLIPWithAdapters("tiny", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                         device="cpu")
+    with pytest.raises(ValueError, match="empty parameter list"):
+        CLIPAdapterTrainer(m, [], output_dir="/tmp/clipmi_t")
+
+
+def test_arena_layout_fused_qkv_is_contiguous():
+    from clipmi.modules import CLIPParams
+    m = CLIPParams(C.resolve("tiny"), "cpu", shadow=False)
+    a = m.arena
+    q = a.offsets["vision_model.encoder.layers.1.self_attn.q_proj.weight"][0]
+    v = a.offsets["vision_model.encoder.layers.1.self_attn.v_proj.weight"][0]
+    D = 128
+    assert v - q == 2 * D * D
+    for name, (off, _, _) in a.offsets.items():
+        assert off % 8 == 0, name
+    # parameters are views of the arena: an in-place update shows in the flat buffer
+    with torch.no_grad():
+        m.vision_model.encoder.layers[1].self_attn.k_proj.weight.fill_(3.0)
+    assert a.data[q + D * D: q + 2 * D * D].eq(3.0).all()
+
+
+def test_flops_model_matches_survey():
+    assert abs(C.forward_flops_per_pair(C.resolve("B/16")) / 1e9 - 41.086) < 0.01
+    assert abs(C.forward_flops_per_pair(C.resolve("B/32")) / 1e9 - 14.777) < 0.01
+    assert abs(C.forward_flops_per_pair(C.resolve("L/14")) / 1e9 - 175.325) < 0.01
+
+
+def test_synthetic_batch_sharding_is_consistent():
+    cfg = C.resolve("tiny")
+    full = synth.synthetic_batch(cfg, 6, seed=7)
+    a = synth.synthetic_batch(cfg, 3, seed=7, start=0)
+    b = synth.synthetic_batch(cfg, 3, seed=7, start=3)
+    for k in full:
+        assert np.array_equal(full[k], np.concatenate([a[k], b[k]]))
+    ids, mask = full["input_ids"], full["attention_mask"]
+    assert (ids[:, 0] == cfg.text_config.bos_token_id).all()
+    L = mask.sum(1)
+    assert ((L >= 5) & (L <= 77)).all()
+
+
+def _dp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    from clipmi import towers as T
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    Bg, E = 8, 16
+    tg = torch.randn(Bg, E, dtype=torch.float64)
+    ig = torch.randn(Bg, E, dtype=torch.float64)
+    s = torch.tensor(2.0, dtype=torch.float64)
+    B = Bg // world
+    tl = tg[rank * B:(rank + 1) * B].clone().requires_grad_(True)
+    il = ig[rank * B:(rank + 1) * B].clone().requires_grad_(True)
+    # the same decomposition ContrastiveFn runs, with its collective helpers
+    th, ih = tl / tl.norm(dim=-1, keepdim=True), il / il.norm(dim=-1, keepdim=True)
+    tall = T._gather(th.detach(), None, world)
+    iall = T._gather(ih.detach(), None, world)
+    lab = torch.arange(B) + rank * B
+    lt = s.exp() * th @ iall.t()
+    li = s.exp() * ih @ tall.t()
+    loss = (F.cross_entropy(lt, lab, reduction="sum") + F.cross_entropy(li, lab, reduction="sum")) / (2 * Bg)
+    loss.backward()
+    # column-direction gradient terms: d loss / d (gathered features), reduce-scattered to owners
+    tall_r = tall.clone().requires_grad_(True)
+    iall_r = iall.clone().requires_grad_(True)
+    l2 = (F.cross_entropy(s.exp() * th.detach() @ iall_r.t(), lab, reduction="sum")
+          + F.cross_entropy(s.exp() * ih.detach() @ tall_r.t(), lab, reduction="sum")) / (2 * Bg)
+    l2.backward()
+    gt_extra = T._reduce_scatter(tall_r.grad, None, world)
+    gi_extra = T._reduce_scatter(iall_r.grad, None, world)
+    # chain the extra normalized-feature gradient through the local normalisation
+    th2 = tl.detach().clone().requires_grad_(True)
+    (th2 / th2.norm(dim=-1, keepdim=True)).backward(gt_extra)
+    ih2 = il.detach().clone().requires_grad_(True)
+    (ih2 / ih2.norm(dim=-1, keepdim=True)).backward(gi_extra)
+    lsum = loss.detach().clone()
+    dist.all_reduce(lsum)
+    q.put((rank, lsum.item(), (tl.grad + th2.grad).numpy(), (il.grad + ih2.grad).numpy()))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_contrastive_decomposition_gloo():
+    """Sum over 2 ranks of the sharded loss == single-device loss; sharded feature grads ==
+    single-device grads."""
+    import torch.multiprocessing as mp
+    import torch.nn.functional as F
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+    torch.manual_seed(0)
+    Bg, E = 8, 16
+    tg = torch.randn(Bg, E, dtype=torch.float64, requires_grad=True)
+    ig = torch.randn(Bg, E, dtype=torch.float64, requires_grad=True)
+    s = torch.tensor(2.0, dtype=torch.float64)
+    L = s.exp() * (tg / tg.norm(dim=-1, keepdim=True)) @ (ig / ig.norm(dim=-1, keepdim=True)).t()
+    lab = torch.arange(Bg)
+    ref = (F.cross_entropy(L, lab) + F.cross_entropy(L.t(), lab)) / 2
+    ref.backward()
+    for rank, lsum, gt, gi in res:
+        assert abs(lsum - ref.item()) < 1e-12
+        np.testing.assert_allclose(gt, tg.grad[rank * 4:(rank + 1) * 4].numpy(), atol=1e-12)
+        np.testing.assert_allclose(gi, ig.grad[rank * 4:(rank + 1) * 4].numpy(), atol=1e-12)

@@ -1,0 +1,245 @@
+"""Per-kernel parity of libclipmi against plain PyTorch fp32 references of the same op:
+LayerNorm (+ fused vision embedding add), attention fwd/bwd (causal + key padding and
+bidirectional), embeddings, column sums, contrastive CE, AdamW and grad-norm."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from clipmi import towers as T  # noqa: E402
+from clipmi import kernels as kern  # noqa: E402
+from clipmi._lib import BF16, F32  # noqa: E402
+
+DT = {torch.bfloat16: BF16, torch.float32: F32}
+TOL = {torch.bfloat16: 3e-2, torch.float32: 2e-5}
+
+
+def rnd(shape, seed, dtype=torch.float32, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to("cuda", dtype)
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("D", [128, 512, 768, 1024])
+def test_layernorm_fwd_bwd(dtype, D):
+    R = 333
+    x = rnd((R, D), 1, dtype)
+    w = rnd((D,), 2, dtype, 0.2) + 1
+    b = rnd((D,), 3, dtype, 0.2)
+    y = torch.empty_like(x)
+    st = torch.empty(2, R, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_layernorm_fwd", s, DT[dtype], x.data_ptr(), D, y.data_ptr(), D, w.data_ptr(), b.data_ptr(),
+           st[0].data_ptr(), st[1].data_ptr(), R, D, 1e-5, None, None, 0)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = b.float().requires_grad_(True)
+    yr = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    assert rel(y, yr) < TOL[dtype]
+    dy = rnd((R, D), 4, dtype)
+    dres = rnd((R, D), 5, dtype)
+    yr.backward(dy.float())
+    dx = torch.empty_like(x)
+    dw = torch.zeros(D, device="cuda")
+    db = torch.zeros(D, device="cuda")
+    ws = torch.empty(int(T._lib.lib().clipmi_layernorm_bwd_ws(R, D)), dtype=torch.uint8, device="cuda")
+    T.call("clipmi_layernorm_bwd", s, DT[dtype], dy.data_ptr(), D, x.data_ptr(), D, st[0].data_ptr(),
+           st[1].data_ptr(), w.data_ptr(), dx.data_ptr(), D, dres.data_ptr(), D, dw.data_ptr(), db.data_ptr(), 1,
+           ws.data_ptr(), ws.numel(), R, D)
+    assert rel(dx, xr.grad + dres.float()) < TOL[dtype] * 2
+    assert rel(dw, wr.grad) < TOL[dtype] * 2
+    assert rel(db, br.grad) < TOL[dtype] * 2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm_vision_embed_fused(dtype):
+    B, N, D = 3, 50, 768
+    h0 = rnd((B * N, D), 6, dtype)
+    pos = rnd((N, D), 7, dtype)
+    cls = rnd((D,), 8, dtype)
+    w = rnd((D,), 9, dtype, 0.1) + 1
+    b = rnd((D,), 10, dtype, 0.1)
+    ref_in = h0.float().view(B, N, D) + pos.float()[None]
+    ref_in[:, 0] += cls.float()
+    y = torch.empty_like(h0)
+    st = torch.empty(2, B * N, device="cuda")
+    T.call("clipmi_layernorm_fwd", kern.stream(), DT[dtype], h0.data_ptr(), D, y.data_ptr(), D, w.data_ptr(),
+           b.data_ptr(), st[0].data_ptr(), st[1].data_ptr(), B * N, D, 1e-5, pos.data_ptr(), cls.data_ptr(), N)
+    assert rel(h0.view(B, N, D), ref_in) < TOL[dtype]
+    assert rel(y.view(B, N, D), F.layer_norm(ref_in, (D,), w.float(), b.float(), 1e-5)) < TOL[dtype]
+
+
+def attn_ref(qkv, B, N, H, mask, causal):
+    D = H * 64
+    q, k, v = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / 8.0
+    blocked = torch.zeros(B, 1, N, N, dtype=torch.bool, device=qkv.device)
+    if causal:
+        blocked |= torch.triu(torch.ones(N, N, dtype=torch.bool, device=qkv.device), 1)
+    if mask is not None:
+        blocked |= (mask == 0)[:, None, None, :]
+    s = s.masked_fill(blocked, float("-inf"))
+    p = torch.softmax(s, -1)
+    o = (p @ v).transpose(1, 2).reshape(B * N, D)
+    return o, torch.logsumexp(s, -1).reshape(-1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 50, 12, False), (2, 197, 12, False),
+                                           (3, 77, 8, True), (2, 256, 2, False)])
+def test_attention(dtype, B, N, H, causal):
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 11, dtype)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(12)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    o = torch.empty(B * N, D, dtype=dtype, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_attention_fwd", s, DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(),
+           mask.data_ptr() if mask is not None else None, int(causal), B, H, N, D)
+    qr = qkv.float().requires_grad_(True)
+    oref, lref = attn_ref(qr, B, N, H, mask, causal)
+    assert rel(o, oref) < TOL[dtype], "O"
+    assert (lse - lref).abs().max().item() < (2e-2 if dtype == torch.bfloat16 else 1e-4), "lse"
+    do = rnd((B * N, D), 13, dtype)
+    oref.backward(do.float())
+    dqkv = torch.empty_like(qkv)
+    T.call("clipmi_attention_bwd", s, DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+           dqkv.data_ptr(), mask.data_ptr() if mask is not None else None, int(causal), B, H, N, D)
+    g = qr.grad
+    for i, nm in enumerate("qkv"):
+        sl = slice(i * D, (i + 1) * D)
+        assert rel(dqkv[:, sl], g[:, sl]) < TOL[dtype] * 2, nm
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_text_embedding_fwd_bwd(dtype):
+    B, S, D, V = 6, 77, 512, 1000
+    g = torch.Generator().manual_seed(14)
+    ids = torch.randint(0, V, (B, S), generator=g)
+    ids[:, 40:] = V - 1  # heavy repetition, like EOS padding
+    ids = ids.cuda()
+    tok = rnd((V, D), 15, dtype)
+    pos = rnd((S, D), 16, dtype)
+    x0 = torch.empty(B * S, D, dtype=dtype, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_text_embed", s, DT[dtype], ids.data_ptr(), tok.data_ptr(), pos.data_ptr(), x0.data_ptr(),
+           B * S, S, D, V, bad.data_ptr())
+    ref = tok.float()[ids] + pos.float()[None]
+    assert rel(x0.view(B, S, D), ref) < TOL[dtype]
+    assert bad.item() == 0
+    dx = rnd((B * S, D), 17, dtype)
+    gtok = torch.zeros(V, D, device="cuda")
+    ws = torch.empty(int(T._lib.lib().clipmi_text_embed_bwd_ws(B * S, V)), dtype=torch.uint8, device="cuda")
+    T.call("clipmi_text_embed_bwd", s, DT[dtype], ids.data_ptr(), dx.data_ptr(), B * S, D, V, gtok.data_ptr(), 1,
+           ws.data_ptr(), ws.numel())
+    gref = torch.zeros(V, D, device="cuda").index_add_(0, ids.view(-1), dx.float())
+    assert rel(gtok, gref) < 1e-5
+    gpos = torch.zeros(S, D, device="cuda")
+    T.call("clipmi_period_sum", s, DT[dtype], dx.data_ptr(), D, B, S, S, D, gpos.data_ptr(), 1)
+    assert rel(gpos, dx.float().view(B, S, D).sum(0)) < 1e-5
+    ids_bad = ids.clone()
+    ids_bad[0, 3] = V + 5
+    T.call("clipmi_text_embed", s, DT[dtype], ids_bad.data_ptr(), tok.data_ptr(), pos.data_ptr(), x0.data_ptr(),
+           B * S, S, D, V, bad.data_ptr())
+    assert bad.item() == 1
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_im2col_matches_conv(dtype):
+    B, H, P, D = 2, 64, 16, 128
+    px = rnd((B, 3, H, H), 18)
+    W = rnd((D, 3, P, P), 19, scale=0.05)
+    G = H // P
+    Kp = 3 * P * P
+    X = torch.empty(B * (G * G + 1), Kp, dtype=dtype, device="cuda")
+    T.call("clipmi_im2col", kern.stream(), DT[dtype], px.data_ptr(), X.data_ptr(), B, 3, H, P, Kp)
+    out = torch.empty(B * (G * G + 1), D, dtype=torch.float32, device="cuda")
+    Wd = W.to(dtype).view(D, Kp).contiguous()
+    kern.gemm(B * (G * G + 1), D, Kp, X, Kp, True, Wd, Kp, True, out, D)
+    ref = F.conv2d(px, W, stride=P).flatten(2).transpose(1, 2)
+    out = out.view(B, G * G + 1, D)
+    assert out[:, 0].abs().max().item() == 0.0
+    assert rel(out[:, 1:], ref) < TOL[dtype]
+
+
+def test_colsum():
+    R, N = 5000, 3072
+    x = rnd((R, N), 20, torch.bfloat16)
+    out = rnd((N,), 21)
+    o0 = out.clone()
+    ws = torch.empty(int(T._lib.lib().clipmi_colsum_ws(R, N)), dtype=torch.uint8, device="cuda")
+    T.call("clipmi_colsum", kern.stream(), BF16, x.data_ptr(), N, R, N, out.data_ptr(), 1, ws.data_ptr(), ws.numel())
+    assert rel(out, o0 + x.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("B,E", [(8, 64), (256, 512), (1000, 512)])
+def test_contrastive_fn_matches_torch(B, E):
+    t = rnd((B, E), 22).requires_grad_(True)
+    i = rnd((B, E), 23).requires_grad_(True)
+    ls = torch.tensor(math.log(100.0), device="cuda", requires_grad=True)
+
+    class _A:  # minimal arena stand-in for the logit_scale gradient
+        def __init__(self):
+            self.grad = torch.zeros(64, device="cuda")
+
+        def prepare_grads(self):
+            pass
+
+        def ptr(self, name, buf):
+            return buf.data_ptr()
+
+    ar = _A()
+    loss, th, ih, lt, li = T.ContrastiveFn.apply(t, i, ls, None, True, ar)
+    loss.backward()
+    tr = t.detach().clone().requires_grad_(True)
+    ir = i.detach().clone().requires_grad_(True)
+    lr_ = ls.detach().clone().requires_grad_(True)
+    tn, inn = tr / tr.norm(dim=-1, keepdim=True), ir / ir.norm(dim=-1, keepdim=True)
+    L = tn @ inn.t() * lr_.exp()
+    lab = torch.arange(B, device="cuda")
+    lref = (F.cross_entropy(L, lab) + F.cross_entropy(L.t(), lab)) / 2
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-5
+    assert rel(lt, L) < 1e-5
+    assert rel(li, L.t()) < 1e-5
+    assert rel(t.grad, tr.grad) < 1e-4
+    assert rel(i.grad, ir.grad) < 1e-4
+    assert abs(ar.grad[0].item() - lr_.grad.item()) < 1e-4 * max(1, abs(lr_.grad.item()))
+
+
+def test_adamw_and_clip_match_torch():
+    n = 100_003
+    p = rnd((n,), 24)
+    g = rnd((n,), 25, scale=3.0)
+    p_ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([p_ref], lr=1e-3, weight_decay=0.01)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    shadow = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    norm = torch.zeros(2, device="cuda")
+    gp = (T.c_vp * 1)(g.data_ptr())
+    gn = (T.c_i64 * 1)(n)
+    ws = torch.empty(int(T._lib.lib().clipmi_grad_norm_multi_ws(1)), dtype=torch.uint8, device="cuda")
+    for step in range(1, 4):
+        T.call("clipmi_grad_norm_multi", kern.stream(), gp, gn, 1, 1.0, norm.data_ptr(), ws.data_ptr(), ws.numel())
+        T.call("clipmi_adamw", kern.stream(), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+               shadow.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, norm.data_ptr())
+        p_ref.grad = g.clone()
+        tn = torch.nn.utils.clip_grad_norm_([p_ref], 1.0)
+        opt.step()
+        assert abs(norm[0].item() - tn.item()) < 1e-3 * tn.item()
+    assert rel(p, p_ref.detach()) < 1e-5
+    assert rel(shadow, p_ref.detach()) < 1e-2

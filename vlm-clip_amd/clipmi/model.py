@@ -1,0 +1,249 @@
+"""Drop-in ``CLIPWithAdapters`` (model_m.py:10-248) on the MI355X-native kernels.
+
+Same constructor arguments, forward signature, return dicts, feature methods, adapter
+checkpoint format and error types as the reference; the compute runs on libclipmi
+(``clipmi.towers``).  Extensions, all keyword-only:
+
+  device       where the fp32 parameter arenas live (default: cuda if available)
+  precision    "bf16" (MFMA path, default) or "fp32" (exact-f32 parity mode)
+  pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
+               (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
+  init_seed    seed of the deterministic random init used when no weights file exists
+  process_group torch.distributed group for the data-parallel contrastive loss
+"""
+from __future__ import annotations
+
+import os
+import warnings
+
+import torch
+import torch.nn as nn
+
+from . import config as C
+from . import synth
+from . import towers as T
+from .modules import AdapterParams, CLIPParams
+
+
+class _Runtime:
+    def __init__(self, clip: CLIPParams, dtype):
+        self.arena = clip.arena
+        self.cfg = clip.config
+        self.dtype = dtype
+        self.venc = T.Encoder(self.arena, "vision_model", self.cfg.vision_config, causal=False)
+        self.tenc = T.Encoder(self.arena, "text_model", self.cfg.text_config, causal=True)
+        self.train_tower = False
+        self.bad_flag = torch.zeros(1, dtype=torch.int32, device=self.arena.device)
+
+
+def _anchor(module: nn.Module):
+    for p in module.parameters():
+        if p.requires_grad:
+            return p
+    return next(module.parameters())
+
+
+class CLIPWithAdapters(nn.Module):
+    """CLIP model with text and vision adapters (model_m.py:10-248)."""
+
+    def __init__(self, clip_model_name="openai/clip-vit-base-patch32", text_adapter_size=256,
+                 vision_adapter_size=256, shared_adapter_layers=2, freeze_clip=True, use_text_adapter=True,
+                 use_vision_adapter=True, use_shared_adapters=True, *, device=None, precision="bf16",
+                 pooling="first", init_seed=0, process_group=None):
+        super().__init__()
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be 'bf16' or 'fp32'")
+        if pooling not in ("first", "eos"):
+            raise ValueError("pooling must be 'first' or 'eos'")
+        cfg = C.resolve(clip_model_name)
+        self.config = cfg
+        self.precision = precision
+        self.pooling = pooling
+        self.process_group = process_group
+        dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+        shadow = precision == "bf16"
+        # model_m.py:29-30 — CLIPModel.from_pretrained / CLIPProcessor.from_pretrained
+        self.clip = CLIPParams(cfg, device, shadow)
+        self.clip.text_model.config = cfg.text_config
+        self.clip.vision_model.config = cfg.vision_config
+        self.processor = None  # tokenizer/image transform are host I/O, out of scope
+        self._load_clip_weights(clip_model_name, init_seed)
+        text_hidden = cfg.text_config.hidden_size
+        vision_hidden = cfg.vision_config.hidden_size
+        self.use_text_adapter = use_text_adapter
+        self.use_vision_adapter = use_vision_adapter
+        self.use_shared_adapters = use_shared_adapters
+        self.text_adapter = None
+        self.vision_adapter = None
+        self.shared_adapters = None
+        if use_text_adapter:
+            self.text_adapter = AdapterParams(text_hidden, text_adapter_size, device, shadow=shadow)
+            self.text_adapter.load_numpy(synth.adapter_state_dict(text_hidden, text_adapter_size, init_seed,
+                                                                  "text_adapter"))
+        if use_vision_adapter:
+            self.vision_adapter = AdapterParams(vision_hidden, vision_adapter_size, device, shadow=shadow)
+            self.vision_adapter.load_numpy(synth.adapter_state_dict(vision_hidden, vision_adapter_size, init_seed,
+                                                                    "vision_adapter"))
+        if use_shared_adapters:
+            warnings.warn("use_shared_adapters=True: the reference's SharedMHSAttentionAdapter path crashes for "
+                          "batch > 1 (model_m.py:96-98, SURVEY quirk Q3) and is not on the accelerated path yet; "
+                          "forward() will raise. Pass use_shared_adapters=False.", stacklevel=2)
+        self._rt = _Runtime(self.clip, dtype)
+        if freeze_clip:
+            self._freeze_clip_parameters()
+
+    # ------------------------------------------------------------------ weights
+    def _load_clip_weights(self, name, seed):
+        path = os.path.join(str(name), "model.safetensors")
+        if os.path.isfile(path):
+            from safetensors.torch import load_file
+            sd = load_file(path, device="cpu")
+            sd = {k: v for k, v in sd.items() if not k.endswith("position_ids")}
+            missing = [k for k in self.clip.arena.params if k not in sd]
+            if missing:
+                raise ValueError(f"checkpoint {path} misses {missing[:4]}...")
+            self.clip.load_numpy(sd)
+        else:
+            self.clip.load_numpy(synth.clip_state_dict(self.config, seed=seed))
+
+    def _freeze_clip_parameters(self):
+        """model_m.py:67-70."""
+        for param in self.clip.parameters():
+            param.requires_grad = False
+
+    def _unfreeze_clip_parameters(self):
+        """model_m.py:72-75 (also makes logit_scale trainable: SURVEY quirk Q4)."""
+        for param in self.clip.parameters():
+            param.requires_grad = True
+
+    @property
+    def dtype(self):
+        return self._rt.dtype
+
+    def arenas(self):
+        out = [self.clip.arena]
+        for a in (self.text_adapter, self.vision_adapter):
+            if a is not None:
+                out.append(a.arena)
+        return out
+
+    # ------------------------------------------------------------------ features
+    def _tower_training(self):
+        return torch.is_grad_enabled() and self.clip.arena.any_requires_grad()
+
+    def _adapter_needs_grad(self, mod, x):
+        return torch.is_grad_enabled() and (mod.arena.any_requires_grad() or x.requires_grad)
+
+    def _check_device(self, t):
+        if t.device != self.clip.arena.device:
+            t = t.to(self.clip.arena.device, non_blocking=True)
+        return t
+
+    def text_hidden_states(self, input_ids, attention_mask=None):
+        self._rt.train_tower = self._tower_training()
+        ids = self._check_device(input_ids)
+        mask = self._check_device(attention_mask) if attention_mask is not None else None
+        h = T.TextTowerFn.apply(ids, mask, _anchor(self.clip), self._rt)
+        if self.use_text_adapter:
+            h = T.AdapterFn.apply(h, _anchor(self.text_adapter), self._rt, self.text_adapter,
+                                  self._adapter_needs_grad(self.text_adapter, h))
+        return h
+
+    def get_text_features(self, input_ids, attention_mask):
+        """model_m.py:77-105: text tower -> adapter -> token 0 -> text_projection."""
+        if self.use_shared_adapters:
+            raise NotImplementedError("shared adapters (model_m.py:95-100) are not supported: the reference "
+                                      "crashes for batch > 1 there (SURVEY quirk Q3)")
+        h = self.text_hidden_states(input_ids, attention_mask)
+        idx = None
+        if self.pooling == "eos":
+            t = self.config.text_config
+            ids = self._check_device(input_ids).to(torch.int64).contiguous()
+            idx = torch.empty(ids.shape[0], dtype=torch.int32, device=ids.device)
+            mode = 2 if t.eos_token_id == 2 else 1
+            T.call("clipmi_pool_index", T.K.stream(), T.P_(ids), ids.shape[0], ids.shape[1], t.eos_token_id, mode,
+                   T.P_(idx))
+        return T.PoolProjFn.apply(h, self.clip.text_projection.weight, self._rt, "text_projection.weight", idx)
+
+    def vision_hidden_states(self, pixel_values):
+        self._rt.train_tower = self._tower_training()
+        px = self._check_device(pixel_values)
+        h = T.VisionTowerFn.apply(px, _anchor(self.clip), self._rt)
+        if self.use_vision_adapter:
+            h = T.AdapterFn.apply(h, _anchor(self.vision_adapter), self._rt, self.vision_adapter,
+                                  self._adapter_needs_grad(self.vision_adapter, h))
+        return h
+
+    def get_image_features(self, pixel_values):
+        """model_m.py:107-125: vision tower (no post-LN, quirk Q2) -> adapter -> CLS -> visual_projection."""
+        h = self.vision_hidden_states(pixel_values)
+        return T.PoolProjFn.apply(h, self.clip.visual_projection.weight, self._rt, "visual_projection.weight", None)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids=None, attention_mask=None, pixel_values=None, return_loss=True):
+        """model_m.py:127-176."""
+        if input_ids is not None and attention_mask is not None:
+            text_features = self.get_text_features(input_ids, attention_mask)
+        else:
+            text_features = None
+        image_features = self.get_image_features(pixel_values) if pixel_values is not None else None
+        if return_loss and text_features is not None and image_features is not None:
+            group = self.process_group
+            loss, t, i, lpt, lpi = T.ContrastiveFn.apply(text_features, image_features, self.clip.logit_scale,
+                                                         group, True, self.clip.arena)
+            world = torch.distributed.get_world_size(group) if group is not None else 1
+            return {"loss": loss, "text_features": t, "image_features": i, "logits_per_text": lpt,
+                    "logits_per_image": lpt.t() if world == 1 else lpi}
+        return {"text_features": text_features, "image_features": image_features}
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_adapter_weights(self, save_path):
+        """model_m.py:178-203 — {"text_adapter": sd, "vision_adapter": sd} via torch.save."""
+        adapter_state_dict = {}
+        if self.use_text_adapter:
+            adapter_state_dict["text_adapter"] = {k: v.detach().clone() for k, v in self.text_adapter.state_dict().items()}
+        if self.use_vision_adapter:
+            adapter_state_dict["vision_adapter"] = {k: v.detach().clone()
+                                                    for k, v in self.vision_adapter.state_dict().items()}
+        if self.use_shared_adapters:
+            raise NotImplementedError("shared adapters are not supported (SURVEY quirk Q3)")
+        if not adapter_state_dict:
+            raise ValueError("No adapters enabled to save")
+        d = os.path.dirname(save_path)
+        if d:  # the reference calls os.makedirs("") for bare file names and crashes
+            os.makedirs(d, exist_ok=True)
+        torch.save(adapter_state_dict, save_path)
+        print(f"Adapter weights saved to {save_path}")
+        print(f"Saved adapters: {list(adapter_state_dict.keys())}")
+
+    def load_adapter_weights(self, load_path):
+        """model_m.py:205-248 (same validation and error types; safe loader only)."""
+        if not os.path.exists(load_path):
+            raise FileNotFoundError(f"No adapter weights found at {load_path}")
+        adapter_state_dict = torch.load(load_path, map_location=self.clip.arena.device, weights_only=True)
+        if "text_adapter" in adapter_state_dict:
+            if not self.use_text_adapter:
+                raise ValueError("Text adapter weights found but text adapter is not enabled")
+            self.text_adapter.load_state_dict(adapter_state_dict["text_adapter"])
+        elif self.use_text_adapter:
+            raise ValueError("Text adapter is enabled but no weights found in checkpoint")
+        if "vision_adapter" in adapter_state_dict:
+            if not self.use_vision_adapter:
+                raise ValueError("Vision adapter weights found but vision adapter is not enabled")
+            self.vision_adapter.load_state_dict(adapter_state_dict["vision_adapter"])
+        elif self.use_vision_adapter:
+            raise ValueError("Vision adapter is enabled but no weights found in checkpoint")
+        if "shared_adapters" in adapter_state_dict:
+            if not self.use_shared_adapters:
+                raise ValueError("Shared adapter weights found but shared adapters are not enabled")
+            raise NotImplementedError("shared adapters are not supported (SURVEY quirk Q3)")
+        elif self.use_shared_adapters:
+            raise ValueError("Shared adapters are enabled but no weights found in checkpoint")
+        print(f"Adapter weights loaded from {load_path}")
+        print(f"Loaded adapters: {list(adapter_state_dict.keys())}")
+
+    def input_error(self) -> bool:
+        """True if any token id seen so far was outside the vocabulary (checked lazily, on device)."""
+        return bool(self._rt.bad_flag.item())

@@ -1,0 +1,569 @@
+"""Autograd functions that run the CLIP path on libclipmi.
+
+Each Function's forward/backward is a short sequence of C-ABI calls (the encoder stack
+is ONE call per direction, sequenced natively in csrc/engine.cpp).  Parameter
+gradients are written straight into the fp32 gradient arena (``Arena.grad``) and exposed
+as ``p.grad`` views (AccumulateGrad semantics emulated by ``Arena.prepare_grads``), so
+autograd only carries activation gradients between the Functions.
+
+Reference mapping:
+  VisionTowerFn  <- CLIPVisionModel.forward ([HF] modeling_clip.py:638-651), last_hidden_state
+                    without post_layernorm (model_m.py:116, quirk Q2)
+  TextTowerFn    <- CLIPTextModel.forward ([HF] :513-559), last_hidden_state after final LN
+  AdapterFn      <- TextAdapter/VisionAdapter.forward (adapter/clip_adapter.py:17-23, 144-150),
+                    peclip.TextualAdapter (adapter/peclip.py:13-18) with ln=False
+  PoolProjFn     <- [:, 0, :] + text_projection / visual_projection (model_m.py:102-103, 122-123)
+  ContrastiveFn  <- model_m.py:146-171 (+ the SURVEY §8e data-parallel all-gather form)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from . import kernels as K
+from ._lib import BF16, F32
+
+c_vp, c_i64, c_int, c_float = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+
+W_FIELDS = ["ln1_w", "ln1_b", "qkv_w", "qkv_b", "out_w", "out_b", "ln2_w", "ln2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b"]
+A_FIELDS = ["x_in", "ln1", "qkv", "o", "h", "ln2", "pre", "act", "mean1", "rstd1", "lse", "mean2", "rstd2"]
+
+
+class LayerW(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in W_FIELDS]
+
+
+class LayerG(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in W_FIELDS]
+
+
+class LayerAct(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in A_FIELDS]
+
+
+class EncoderDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("B", c_int), ("N", c_int), ("D", c_int), ("F", c_int), ("H", c_int),
+                ("L", c_int), ("eps", c_float), ("causal", c_int), ("attention_mask", c_vp),
+                ("layers", ctypes.POINTER(LayerW)), ("grads", ctypes.POINTER(LayerG)),
+                ("act", ctypes.POINTER(LayerAct)), ("x_out", c_vp), ("workspace", c_vp),
+                ("workspace_bytes", c_i64)]
+
+
+P = ctypes.POINTER
+_lib.declare("clipmi_encoder_fwd", [c_vp, P(EncoderDesc)])
+_lib.declare("clipmi_encoder_bwd", [c_vp, P(EncoderDesc), c_vp])
+_lib.declare("clipmi_encoder_bwd_ws", [P(EncoderDesc)], c_i64)
+_lib.declare("clipmi_layernorm_fwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                                      c_float, c_vp, c_vp, c_int])
+_lib.declare("clipmi_layernorm_bwd_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_layernorm_bwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                      c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
+_lib.declare("clipmi_colsum_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_colsum", [c_vp, c_int, c_vp, c_i64, c_int, c_int, c_vp, c_int, c_vp, c_i64])
+_lib.declare("clipmi_period_sum", [c_vp, c_int, c_vp, c_i64, c_int, c_int, c_int, c_int, c_vp, c_int])
+_lib.declare("clipmi_text_embed", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp])
+_lib.declare("clipmi_text_embed_bwd_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_text_embed_bwd", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64])
+_lib.declare("clipmi_im2col", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
+_lib.declare("clipmi_pool_index", [c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp])
+_lib.declare("clipmi_gather_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp])
+_lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int])
+_lib.declare("clipmi_attention_fwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
+_lib.declare("clipmi_attention_bwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                      c_int])
+_lib.declare("clipmi_l2norm_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int])
+_lib.declare("clipmi_l2norm_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int])
+_lib.declare("clipmi_contrastive_ce_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp])
+_lib.declare("clipmi_contrastive_ce_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp])
+_lib.declare("clipmi_sum2", [c_vp, c_vp, c_vp, c_int, c_float, c_vp, c_int])
+_lib.declare("clipmi_cast_f32_bf16", [c_vp, c_vp, c_vp, c_i64])
+_lib.declare("clipmi_grad_norm_ws", [], c_i64)
+_lib.declare("clipmi_grad_norm", [c_vp, c_vp, c_i64, c_float, c_vp, c_vp, c_i64])
+_lib.declare("clipmi_grad_scale", [c_vp, c_vp, c_i64, c_vp])
+_lib.declare("clipmi_grad_norm_multi_ws", [c_int], c_i64)
+_lib.declare("clipmi_grad_norm_multi", [c_vp, P(c_vp), P(c_i64), c_int, c_float, c_vp, c_vp, c_i64])
+_lib.declare("clipmi_adamw", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, c_vp])
+
+
+def call(name, *args):
+    _lib.check(getattr(_lib.lib(), name)(*args), name)
+
+
+def P_(t):
+    return None if t is None else t.data_ptr()
+
+
+def dcode(dtype):
+    return BF16 if dtype == torch.bfloat16 else F32
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------ encoder
+class Encoder:
+    """Binds one tower's encoder layers (an arena prefix) to the native engine."""
+
+    def __init__(self, arena, prefix, tcfg, causal):
+        self.arena, self.prefix, self.t, self.causal = arena, prefix, tcfg, causal
+        self._wcache = {}
+
+    def names(self, i):
+        p = f"{self.prefix}.encoder.layers.{i}"
+        return {"ln1_w": f"{p}.layer_norm1.weight", "ln1_b": f"{p}.layer_norm1.bias",
+                "qkv_w": f"{p}.self_attn.q_proj.weight", "qkv_b": f"{p}.self_attn.q_proj.bias",
+                "out_w": f"{p}.self_attn.out_proj.weight", "out_b": f"{p}.self_attn.out_proj.bias",
+                "ln2_w": f"{p}.layer_norm2.weight", "ln2_b": f"{p}.layer_norm2.bias",
+                "fc1_w": f"{p}.mlp.fc1.weight", "fc1_b": f"{p}.mlp.fc1.bias",
+                "fc2_w": f"{p}.mlp.fc2.weight", "fc2_b": f"{p}.mlp.fc2.bias"}
+
+    def _table(self, cls, buf):
+        key = (cls.__name__, buf.data_ptr(), buf.dtype)
+        tab = self._wcache.get(key)
+        if tab is None:
+            L = self.t.num_hidden_layers
+            tab = (cls * L)()
+            for i in range(L):
+                for f, n in self.names(i).items():
+                    setattr(tab[i], f, self.arena.ptr(n, buf))
+            self._wcache[key] = tab
+        return tab
+
+    def weights(self, wbuf):
+        return self._table(LayerW, wbuf)
+
+    def grads(self):
+        return self._table(LayerG, self.arena.grad)
+
+    def alloc(self, B, N, dtype, device, train):
+        """Activation storage: per-layer for training, one shared set for inference."""
+        t = self.t
+        R, D, F, H, L = B * N, t.hidden_size, t.intermediate_size, t.num_attention_heads, t.num_hidden_layers
+        es = 2 if dtype == torch.bfloat16 else 4
+        al = lambda n: (n + 255) // 256 * 256  # noqa: E731
+        parts = [("x_in", R * D * es), ("ln1", R * D * es), ("qkv", R * 3 * D * es), ("o", R * D * es),
+                 ("h", R * D * es), ("ln2", R * D * es), ("act", R * F * es),
+                 ("mean1", R * 4), ("rstd1", R * 4), ("lse", B * H * N * 4), ("mean2", R * 4), ("rstd2", R * 4)]
+        if train:
+            parts.append(("pre", R * F * es))
+        per = sum(al(n) for _, n in parts)
+        nsets = L if train else 1
+        buf = torch.empty(per * nsets + 256, dtype=torch.uint8, device=device)
+        acts = (LayerAct * L)()
+        base = (buf.data_ptr() + 255) // 256 * 256
+        for i in range(L):
+            off = base + per * (i if train else 0)
+            for name, n in parts:
+                setattr(acts[i], name, off)
+                off += al(n)
+            if not train:
+                acts[i].pre = None
+        return buf, acts
+
+    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None):
+        t = self.t
+        d = EncoderDesc()
+        d.dtype, d.B, d.N, d.D, d.F = dcode(dtype), B, N, t.hidden_size, t.intermediate_size
+        d.H, d.L, d.eps, d.causal = t.num_attention_heads, t.num_hidden_layers, t.layer_norm_eps, int(self.causal)
+        d.attention_mask = P_(mask)
+        d.layers = self.weights(wbuf)
+        d.grads = grads
+        d.act = acts
+        d.x_out = x_out
+        if ws is not None:
+            d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        return d
+
+
+def _wbuf(arena, dtype):
+    if dtype == torch.bfloat16:
+        arena.sync_shadow()
+        return arena.shadow
+    return arena.data
+
+
+# ------------------------------------------------------------------------------ vision
+class VisionTowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pixel_values, anchor, runtime):
+        rt = runtime
+        arena, v, dtype = rt.arena, rt.cfg.vision_config, rt.dtype
+        B = pixel_values.shape[0]
+        if pixel_values.dim() != 4 or pixel_values.shape[1] != v.num_channels:
+            raise ValueError(f"pixel_values must be [B, {v.num_channels}, H, W]")
+        H, W = pixel_values.shape[2], pixel_values.shape[3]
+        if H != v.image_size or W != v.image_size:
+            raise ValueError(f"Input image size ({H}*{W}) doesn't match model ({v.image_size}*{v.image_size}).")
+        dev = pixel_values.device
+        px = pixel_values.to(torch.float32).contiguous()
+        N, D, Pp = v.num_positions, v.hidden_size, v.patch_size
+        Kp = v.num_channels * Pp * Pp
+        if Kp % 8:
+            raise NotImplementedError("patch K = 3*P*P must be a multiple of 8 (P=14 lands next round)")
+        R = B * N
+        train = rt.train_tower
+        s = K.stream()
+        wbuf = _wbuf(arena, dtype)
+        dc = dcode(dtype)
+        X = torch.empty(R, Kp, dtype=dtype, device=dev)
+        call("clipmi_im2col", s, dc, P_(px), P_(X), B, v.num_channels, H, Pp, Kp)
+        h0 = torch.empty(R, D, dtype=dtype, device=dev)
+        K.gemm(R, D, Kp, X, Kp, True, arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kp),
+               Kp, True, h0, D)
+        buf, acts = rt.venc.alloc(B, N, dtype, dev, train)
+        stats0 = torch.empty(2, R, dtype=torch.float32, device=dev)
+        call("clipmi_layernorm_fwd", s, dc, P_(h0), D, acts[0].x_in, D,
+             arena.ptr("vision_model.pre_layrnorm.weight", wbuf), arena.ptr("vision_model.pre_layrnorm.bias", wbuf),
+             P_(stats0[0]), P_(stats0[1]), R, D, v.layer_norm_eps,
+             arena.ptr("vision_model.embeddings.position_embedding.weight", wbuf),
+             arena.ptr("vision_model.embeddings.class_embedding", wbuf), N)
+        out = torch.empty(B, N, D, dtype=dtype, device=dev)
+        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None)
+        _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
+        if train:
+            ctx.rt, ctx.B, ctx.buf, ctx.acts, ctx.X, ctx.h0, ctx.stats0 = rt, B, buf, acts, X, h0, stats0
+        else:
+            del buf
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        rt = ctx.rt
+        arena, v, dtype = rt.arena, rt.cfg.vision_config, rt.dtype
+        B, N, D = ctx.B, v.num_positions, v.hidden_size
+        R = B * N
+        dev = dout.device
+        s = K.stream()
+        dc = dcode(dtype)
+        arena.prepare_grads()
+        wbuf = _wbuf(arena, dtype)
+        dx = dout.to(dtype).contiguous().clone()
+        d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads())
+        ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        _lib.check(_lib.lib().clipmi_encoder_bwd(s, ctypes.byref(d), dx.data_ptr()), "clipmi_encoder_bwd")
+        # pre_layrnorm backward -> gradient of the embedding sum h0
+        dh0 = torch.empty(R, D, dtype=dtype, device=dev)
+        lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
+        g = arena.grad
+        call("clipmi_layernorm_bwd", s, dc, P_(dx), D, P_(ctx.h0), D, P_(ctx.stats0[0]), P_(ctx.stats0[1]),
+             arena.ptr("vision_model.pre_layrnorm.weight", wbuf), P_(dh0), D, None, 0,
+             arena.ptr("vision_model.pre_layrnorm.weight", g), arena.ptr("vision_model.pre_layrnorm.bias", g), 1,
+             P_(lws), lws.numel(), R, D)
+        Kp = ctx.X.shape[1]
+        gW = arena.view("vision_model.embeddings.patch_embedding.weight", g).view(D, Kp)
+        splits = max(1, min(32, 1024 // max(1, ((D + 127) // 128) * ((Kp + 127) // 128))))
+        while splits > 1 and R // splits < 512:
+            splits -= 1
+        wsp = _ws(splits * D * Kp * 4, dev) if splits > 1 else None
+        K.gemm(D, Kp, R, dh0, D, False, ctx.X, Kp, False, gW, Kp, flags=_lib.EPI_BETA, split_k=splits,
+               workspace=wsp)
+        call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
+             arena.ptr("vision_model.embeddings.position_embedding.weight", g), 1)
+        call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, 1, D, arena.ptr("vision_model.embeddings.class_embedding", g), 1)
+        return None, None, None
+
+
+# ------------------------------------------------------------------------------ text
+class TextTowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input_ids, attention_mask, anchor, runtime):
+        rt = runtime
+        arena, t, dtype = rt.arena, rt.cfg.text_config, rt.dtype
+        B, S = input_ids.shape
+        if S > t.max_position_embeddings:
+            raise ValueError(f"Sequence length must be less than max_position_embeddings (got `sequence length`: "
+                             f"{S} and max_position_embeddings: {t.max_position_embeddings}")
+        dev = input_ids.device
+        ids = input_ids.to(torch.int64).contiguous()
+        mask = attention_mask.to(device=dev, dtype=torch.int64).contiguous() if attention_mask is not None else None
+        D = t.hidden_size
+        R = B * S
+        train = rt.train_tower
+        s = K.stream()
+        dc = dcode(dtype)
+        wbuf = _wbuf(arena, dtype)
+        buf, acts = rt.tenc.alloc(B, S, dtype, dev, train)
+        bad = rt.bad_flag
+        call("clipmi_text_embed", s, dc, P_(ids), arena.ptr("text_model.embeddings.token_embedding.weight", wbuf),
+             arena.ptr("text_model.embeddings.position_embedding.weight", wbuf), acts[0].x_in, R, S, D, t.vocab_size,
+             P_(bad))
+        xL = torch.empty(R, D, dtype=dtype, device=dev)
+        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask)
+        _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
+        out = torch.empty(B, S, D, dtype=dtype, device=dev)
+        stats = torch.empty(2, R, dtype=torch.float32, device=dev)
+        call("clipmi_layernorm_fwd", s, dc, P_(xL), D, P_(out), D, arena.ptr("text_model.final_layer_norm.weight", wbuf),
+             arena.ptr("text_model.final_layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, D, t.layer_norm_eps,
+             None, None, 0)
+        if train:
+            ctx.rt, ctx.B, ctx.S, ctx.buf, ctx.acts = rt, B, S, buf, acts
+            ctx.ids, ctx.mask, ctx.xL, ctx.stats = ids, mask, xL, stats
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        rt = ctx.rt
+        arena, t, dtype = rt.arena, rt.cfg.text_config, rt.dtype
+        B, S, D = ctx.B, ctx.S, t.hidden_size
+        R = B * S
+        dev = dout.device
+        s = K.stream()
+        dc = dcode(dtype)
+        arena.prepare_grads()
+        wbuf = _wbuf(arena, dtype)
+        g = arena.grad
+        dy = dout.to(dtype).contiguous()
+        dx = torch.empty(R, D, dtype=dtype, device=dev)
+        lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
+        call("clipmi_layernorm_bwd", s, dc, P_(dy), D, P_(ctx.xL), D, P_(ctx.stats[0]), P_(ctx.stats[1]),
+             arena.ptr("text_model.final_layer_norm.weight", wbuf), P_(dx), D, None, 0,
+             arena.ptr("text_model.final_layer_norm.weight", g), arena.ptr("text_model.final_layer_norm.bias", g), 1,
+             P_(lws), lws.numel(), R, D)
+        d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads())
+        ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        _lib.check(_lib.lib().clipmi_encoder_bwd(s, ctypes.byref(d), dx.data_ptr()), "clipmi_encoder_bwd")
+        V = t.vocab_size
+        ews = _ws(_lib.lib().clipmi_text_embed_bwd_ws(R, V), dev)
+        call("clipmi_text_embed_bwd", s, dc, P_(ctx.ids), P_(dx), R, D, V,
+             arena.ptr("text_model.embeddings.token_embedding.weight", g), 1, P_(ews), ews.numel())
+        call("clipmi_period_sum", s, dc, P_(dx), D, B, S, S, D,
+             arena.ptr("text_model.embeddings.position_embedding.weight", g), 1)
+        return None, None, None, None
+
+
+# ------------------------------------------------------------------------------ adapter
+class AdapterFn(torch.autograd.Function):
+    """y = LN(up(gelu(down(x))) + x)  (ln=False: up(gelu(down(x))) + x)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, runtime, mod, need):
+        arena, dtype = mod.arena, runtime.dtype
+        shp = x.shape
+        Dh, A = mod.hidden, mod.bottleneck
+        x2 = x.to(dtype).reshape(-1, Dh).contiguous()
+        R = x2.shape[0]
+        dev = x.device
+        s = K.stream()
+        dc = dcode(dtype)
+        wbuf = _wbuf(arena, dtype)
+        dn, up = mod.names
+        pre = torch.empty(R, A, dtype=dtype, device=dev) if need else None
+        act = torch.empty(R, A, dtype=dtype, device=dev)
+        flags = _lib.EPI_BIAS | _lib.EPI_GELU | (_lib.EPI_STORE_PRE if need else 0)
+        K.gemm(R, A, Dh, x2, Dh, True, arena.view(f"{dn}.weight", wbuf), Dh, True, act, A,
+               bias=arena.view(f"{dn}.bias", wbuf), aux=pre, ldaux=A, flags=flags)
+        z = torch.empty(R, Dh, dtype=dtype, device=dev)
+        K.gemm(R, Dh, A, act, A, True, arena.view(f"{up}.weight", wbuf), A, True, z, Dh,
+               bias=arena.view(f"{up}.bias", wbuf), residual=x2, ldr=Dh, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
+        if mod.has_ln:
+            y = torch.empty(R, Dh, dtype=dtype, device=dev)
+            stats = torch.empty(2, R, dtype=torch.float32, device=dev)
+            call("clipmi_layernorm_fwd", s, dc, P_(z), Dh, P_(y), Dh, arena.ptr("layer_norm.weight", wbuf),
+                 arena.ptr("layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, Dh, 1e-5, None, None, 0)
+        else:
+            y, stats = z, None
+        if need:
+            ctx.save = (x2, pre, act, z, stats)
+            ctx.mod, ctx.rt, ctx.shape = mod, runtime, shp
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        mod, rt = ctx.mod, ctx.rt
+        x2, pre, act, z, stats = ctx.save
+        arena, dtype = mod.arena, rt.dtype
+        Dh, A = mod.hidden, mod.bottleneck
+        R = x2.shape[0]
+        dev = dy.device
+        s = K.stream()
+        dc = dcode(dtype)
+        train_params = arena.any_requires_grad()
+        if train_params:
+            arena.prepare_grads()
+        g = arena.grad
+        wbuf = _wbuf(arena, dtype)
+        dn, up = mod.names
+        dy2 = dy.to(dtype).reshape(R, Dh).contiguous()
+        if mod.has_ln:
+            dz = torch.empty(R, Dh, dtype=dtype, device=dev)
+            lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, Dh), dev)
+            call("clipmi_layernorm_bwd", s, dc, P_(dy2), Dh, P_(z), Dh, P_(stats[0]), P_(stats[1]),
+                 arena.ptr("layer_norm.weight", wbuf), P_(dz), Dh, None, 0,
+                 arena.ptr("layer_norm.weight", g) if train_params else None,
+                 arena.ptr("layer_norm.bias", g) if train_params else None, 1, P_(lws), lws.numel(), R, Dh)
+        else:
+            dz = dy2
+        cws = _ws(_lib.lib().clipmi_colsum_ws(R, max(Dh, A)), dev)
+        if train_params:
+            K.gemm(Dh, A, R, dz, Dh, False, act, A, False, arena.view(f"{up}.weight", g), A, flags=_lib.EPI_BETA)
+            call("clipmi_colsum", s, dc, P_(dz), Dh, R, Dh, arena.ptr(f"{up}.bias", g), 1, P_(cws), cws.numel())
+        dpre = torch.empty(R, A, dtype=dtype, device=dev)
+        K.gemm(R, A, Dh, dz, Dh, True, arena.view(f"{up}.weight", wbuf), A, False, dpre, A, aux=pre, ldaux=A,
+               flags=_lib.EPI_DGELU)
+        if train_params:
+            K.gemm(A, Dh, R, dpre, A, False, x2, Dh, False, arena.view(f"{dn}.weight", g), Dh, flags=_lib.EPI_BETA)
+            call("clipmi_colsum", s, dc, P_(dpre), A, R, A, arena.ptr(f"{dn}.bias", g), 1, P_(cws), cws.numel())
+        dx = torch.empty(R, Dh, dtype=dtype, device=dev)
+        K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
+               flags=_lib.EPI_RESID)
+        return dx.view(ctx.shape), None, None, None, None
+
+
+# ------------------------------------------------------------------------------ pool + projection
+class PoolProjFn(torch.autograd.Function):
+    """features[b] = W @ h[b, idx[b]]  (fp32 out).  idx None -> token 0 (model_m.py:102,122)."""
+
+    @staticmethod
+    def forward(ctx, h, anchor, runtime, wname, idx):
+        arena, dtype = runtime.arena, runtime.dtype
+        B, S, D = h.shape
+        dev = h.device
+        s = K.stream()
+        dc = dcode(dtype)
+        wbuf = _wbuf(arena, dtype)
+        hc = h.to(dtype).contiguous()
+        pooled = torch.empty(B, D, dtype=dtype, device=dev)
+        call("clipmi_gather_rows", s, dc, P_(hc), P_(idx), B, S, D, P_(pooled))
+        W = arena.view(wname, wbuf)
+        E = W.shape[0]
+        out = torch.empty(B, E, dtype=torch.float32, device=dev)
+        K.gemm(B, E, D, pooled, D, True, W, D, True, out, E)
+        ctx.save = (pooled, idx)
+        ctx.rt, ctx.wname, ctx.shape = runtime, wname, (B, S, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        rt = ctx.rt
+        arena, dtype = rt.arena, rt.dtype
+        pooled, idx = ctx.save
+        B, S, D = ctx.shape
+        dev = dout.device
+        s = K.stream()
+        dc = dcode(dtype)
+        wbuf = _wbuf(arena, dtype)
+        W = arena.view(ctx.wname, wbuf)
+        E = W.shape[0]
+        d = dout.to(torch.float32).contiguous()
+        if dtype == torch.bfloat16:
+            d16 = torch.empty(B, E, dtype=dtype, device=dev)
+            call("clipmi_cast_f32_bf16", s, P_(d), P_(d16), B * E)
+            d = d16
+        if arena.params[ctx.wname].requires_grad:
+            arena.prepare_grads()
+            K.gemm(E, D, B, d, E, False, pooled, D, False, arena.view(ctx.wname, arena.grad), D, flags=_lib.EPI_BETA)
+        dpooled = torch.empty(B, D, dtype=dtype, device=dev)
+        K.gemm(B, D, E, d, E, True, W, D, False, dpooled, D)
+        dh = torch.zeros(B, S, D, dtype=dtype, device=dev)
+        call("clipmi_scatter_rows", s, dc, P_(dpooled), P_(idx), B, S, D, P_(dh), 0)
+        return dh, None, None, None, None
+
+
+# ------------------------------------------------------------------------------ contrastive
+def _gather(x, group, world):
+    if world == 1:
+        return x
+    out = torch.empty(world * x.shape[0], *x.shape[1:], dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
+
+
+def _reduce_scatter(x, group, world):
+    if world == 1:
+        return x
+    out = torch.empty(x.shape[0] // world, *x.shape[1:], dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x.contiguous(), group=group)
+    return out
+
+
+class ContrastiveFn(torch.autograd.Function):
+    """Symmetric InfoNCE.  Single device: exactly model_m.py:146-171.  With a process group
+    of W ranks: all-gather the normalised features, each rank scores its B rows
+    against all Bg = W*B columns with label offset rank*B, loss normalised by 2*Bg (so the
+    all-reduced sum is the global loss), feature gradients reduce-scattered back."""
+
+    @staticmethod
+    def forward(ctx, tf, imf, logit_scale, group, global_loss, arena):
+        world = dist.get_world_size(group) if group is not None else 1
+        rank = dist.get_rank(group) if group is not None else 0
+        B, E = tf.shape
+        dev = tf.device
+        s = K.stream()
+        t = tf.to(torch.float32).contiguous()
+        i = imf.to(torch.float32).contiguous()
+        th, ih = torch.empty_like(t), torch.empty_like(i)
+        tn = torch.empty(B, dtype=torch.float32, device=dev)
+        inn = torch.empty(B, dtype=torch.float32, device=dev)
+        call("clipmi_l2norm_fwd", s, P_(t), P_(th), P_(tn), B, E)
+        call("clipmi_l2norm_fwd", s, P_(i), P_(ih), P_(inn), B, E)
+        tg, ig = _gather(th, group, world), _gather(ih, group, world)
+        Bg = tg.shape[0]
+        lt = torch.empty(B, Bg, dtype=torch.float32, device=dev)
+        li = torch.empty(B, Bg, dtype=torch.float32, device=dev)
+        K.gemm(B, Bg, E, th, E, True, ig, E, True, lt, Bg)   # cos(t_local, i_all)
+        K.gemm(B, Bg, E, ih, E, True, tg, E, True, li, Bg)   # cos(i_local, t_all)
+        lse = torch.empty(2, B, dtype=torch.float32, device=dev)
+        ce = torch.empty(2, B, dtype=torch.float32, device=dev)
+        ls = logit_scale.detach().reshape(1)
+        lab0 = rank * B
+        call("clipmi_contrastive_ce_fwd", s, P_(lt), P_(lt), P_(ls), B, Bg, lab0, P_(lse[0]), P_(ce[0]))
+        call("clipmi_contrastive_ce_fwd", s, P_(li), P_(li), P_(ls), B, Bg, lab0, P_(lse[1]), P_(ce[1]))
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        call("clipmi_sum2", s, P_(ce[0]), P_(ce[1]), B, 1.0 / (2 * Bg), P_(loss), 0)
+        if world > 1 and global_loss:
+            loss_out = loss.clone()
+            dist.all_reduce(loss_out, group=group)
+        else:
+            loss_out = loss
+        ctx.save = (th, ih, tn, inn, tg, ig, lt, li, lse, ls)
+        ctx.group, ctx.world, ctx.B, ctx.Bg, ctx.lab0 = group, world, B, Bg, lab0
+        ctx.ls_param, ctx.arena = logit_scale, arena
+        ctx.mark_non_differentiable(lt, li)
+        return loss_out, th, ih, lt, li
+
+    @staticmethod
+    def backward(ctx, gloss, gth, gih, glt, gli):
+        th, ih, tn, inn, tg, ig, lt, li, lse, ls = ctx.save
+        B, Bg, E, world = ctx.B, ctx.Bg, th.shape[1], ctx.world
+        dev = th.device
+        s = K.stream()
+        gl = gloss.to(torch.float32).contiguous().reshape(1) if gloss is not None else None
+        dSt = torch.empty(B, Bg, dtype=torch.float32, device=dev)
+        dSi = torch.empty(B, Bg, dtype=torch.float32, device=dev)
+        dls = torch.empty(2, B, dtype=torch.float32, device=dev)
+        norm = 1.0 / (2 * Bg)
+        call("clipmi_contrastive_ce_bwd", s, P_(lt), P_(lse[0]), P_(ls), P_(gl), B, Bg, ctx.lab0, norm, P_(dSt), P_(dls[0]))
+        call("clipmi_contrastive_ce_bwd", s, P_(li), P_(lse[1]), P_(ls), P_(gl), B, Bg, ctx.lab0, norm, P_(dSi), P_(dls[1]))
+        # dt^ = dSt i_all + (dSi^T i_local)[rank rows] ; di^ = dSi t_all + (dSt^T t_local)[rank rows]
+        # column-direction terms first (reduce-scattered to their owners), then the row terms
+        # accumulate on top through the GEMM's beta epilogue
+        dTg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
+        dIg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
+        K.gemm(Bg, E, B, dSi, Bg, False, ih, E, False, dTg, E)
+        K.gemm(Bg, E, B, dSt, Bg, False, th, E, False, dIg, E)
+        dth = _reduce_scatter(dTg, ctx.group, world)
+        dih = _reduce_scatter(dIg, ctx.group, world)
+        K.gemm(B, E, Bg, dSt, Bg, True, ig, E, False, dth, E, flags=_lib.EPI_BETA)
+        K.gemm(B, E, Bg, dSi, Bg, True, tg, E, False, dih, E, flags=_lib.EPI_BETA)
+        if gth is not None:
+            dth += gth
+        if gih is not None:
+            dih += gih
+        p = ctx.ls_param
+        if p.requires_grad:
+            # d logit_scale accumulates straight into the grad arena; all ranks' shares are
+            # summed by the data-parallel gradient all-reduce
+            ctx.arena.prepare_grads()
+            call("clipmi_sum2", s, P_(dls[0]), P_(dls[1]), B, 1.0, ctx.arena.ptr("logit_scale", ctx.arena.grad), 1)
+        dt = torch.empty(B, E, dtype=torch.float32, device=dev)
+        di = torch.empty(B, E, dtype=torch.float32, device=dev)
+        call("clipmi_l2norm_bwd", s, P_(dth), P_(th), P_(tn), P_(dt), B, E)
+        call("clipmi_l2norm_bwd", s, P_(dih), P_(ih), P_(inn), P_(di), B, E)
+        return dt, di, None, None, None, None

@@ -1,0 +1,191 @@
+"""Drop-in ``CLIPAdapterTrainer`` (trainer.py:11-167) with a fused, arena-wide optimizer.
+
+The step is the reference's: zero_grad -> loss.backward -> clip_grad_norm_(max_grad_norm)
+-> AdamW.step -> linear warmup/decay scheduler step (trainer.py:91-99,
+[HF] optimization.py:101-129).  Here the clip and the AdamW update are two libclipmi
+launches over the flat fp32 arenas (no per-parameter Python loop, no host sync), and in
+data-parallel runs the gradient arenas are all-reduced (RCCL) once per arena.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from . import kernels as K
+from . import towers as T
+
+
+def linear_schedule_with_warmup(step, warmup, total):
+    """lr multiplier of get_linear_schedule_with_warmup ([HF] optimization.py:101-104)."""
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    return max(0.0, float(total - step) / float(max(1, total - warmup)))
+
+
+class FusedAdamW:
+    """torch.optim.AdamW semantics (decoupled weight decay, bias-corrected) over arenas.
+
+    An arena whose parameters are all trainable is updated by ONE launch; otherwise each
+    trainable parameter's slice gets its own launch of the same kernel."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, arenas=()):
+        params = list(params)
+        if not params:
+            raise ValueError("optimizer got an empty parameter list")
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.step_count = 0
+        ids = {id(p) for p in params}
+        self.segments = []  # (arena, offset, numel)
+        covered = set()
+        for a in arenas:
+            mine = [(n, p) for n, p in a.params.items() if id(p) in ids]
+            if not mine:
+                continue
+            if len(mine) == len(a.params):
+                self.segments.append((a, 0, a.numel))
+            else:
+                for n, p in mine:
+                    off, _, numel = a.offsets[n]
+                    self.segments.append((a, off, numel))
+            covered |= {id(p) for _, p in mine}
+        if covered != ids:
+            raise ValueError("FusedAdamW: every parameter must belong to a clipmi arena")
+        dev = self.segments[0][0].device
+        self.state = [(torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(n, dtype=torch.float32, device=dev))
+                      for _, _, n in self.segments]
+        self.arenas = list({id(a): a for a, _, _ in self.segments}.values())
+        self.norm = torch.zeros(2, dtype=torch.float32, device=dev)
+        n = len(self.segments)
+        self._gp = (ctypes.c_void_p * n)()
+        self._gn = (ctypes.c_int64 * n)()
+        self._norm_ws = torch.empty(int(_lib.lib().clipmi_grad_norm_multi_ws(n)), dtype=torch.uint8, device=dev)
+
+    def zero_grad(self, set_to_none=False):
+        for a in self.arenas:
+            a.zero_grad()
+
+    def grads_all_reduce(self, group=None):
+        """Data-parallel gradient sum: one RCCL all-reduce per arena (bucketed by layout)."""
+        for a in self.arenas:
+            dist.all_reduce(a.grad, group=group)
+
+    def clip_grad_norm(self, max_norm):
+        """norm over all trainable gradients -> self.norm = [total_norm, clip_coef] on device."""
+        for i, (a, off, n) in enumerate(self.segments):
+            self._gp[i] = a.grad.data_ptr() + off * 4
+            self._gn[i] = n
+        T.call("clipmi_grad_norm_multi", K.stream(), self._gp, self._gn, len(self.segments), float(max_norm),
+               T.P_(self.norm), T.P_(self._norm_ws), self._norm_ws.numel())
+        return self.norm[0]
+
+    def step(self, lr=None, clip=True):
+        self.step_count += 1
+        lr = self.lr if lr is None else lr
+        b1, b2 = self.betas
+        s = K.stream()
+        for (a, off, n), (m, v) in zip(self.segments, self.state):
+            shadow = a.shadow.data_ptr() + off * 2 if a.shadow is not None else None
+            T.call("clipmi_adamw", s, a.data.data_ptr() + off * 4, a.grad.data_ptr() + off * 4, T.P_(m), T.P_(v),
+                   shadow, n, lr, b1, b2, self.eps, self.weight_decay, self.step_count,
+                   T.P_(self.norm) if clip else None)
+        for a in self.arenas:
+            a.data._version  # noqa: B018 (our kernel wrote master + shadow together)
+            a.mark_shadow_fresh()
+
+
+class CLIPAdapterTrainer:
+    """trainer.py:11-167.  ``trainable="adapter"`` selects parameters whose name contains
+    "adapter" exactly like trainer.py:40-43; ``trainable="requires_grad"`` takes every
+    parameter with requires_grad (full fine-tune)."""
+
+    def __init__(self, model, train_dataloader, val_dataloader=None, learning_rate=5e-5, weight_decay=0.01,
+                 warmup_steps=0, max_grad_norm=1.0, output_dir="./clip_adapter_checkpoints", *,
+                 trainable="adapter", process_group=None):
+        self.model = model
+        self.train_dataloader = train_dataloader
+        self.val_dataloader = val_dataloader
+        self.learning_rate = learning_rate
+        self.weight_decay = weight_decay
+        self.warmup_steps = warmup_steps
+        self.max_grad_norm = max_grad_norm
+        self.output_dir = output_dir
+        self.process_group = process_group
+        os.makedirs(output_dir, exist_ok=True)
+        self.trainable_params = []
+        for name, param in model.named_parameters():
+            if trainable == "adapter":
+                if "adapter" in name or "shared_adapters" in name:
+                    self.trainable_params.append(param)
+            elif param.requires_grad:
+                self.trainable_params.append(param)
+        self.optimizer = FusedAdamW(self.trainable_params, lr=learning_rate, weight_decay=weight_decay,
+                                    arenas=model.arenas())
+        self.total_steps = None
+
+    def _world(self):
+        if self.process_group is None and not (dist.is_available() and dist.is_initialized()):
+            return 1
+        return dist.get_world_size(self.process_group)
+
+    def train_step(self, batch, step, total_steps):
+        """One reference step (trainer.py:81-99); returns the loss tensor (no host sync)."""
+        device = self.model.clip.arena.device
+        batch = {k: v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v for k, v in batch.items()}
+        outputs = self.model(input_ids=batch.get("input_ids"), attention_mask=batch.get("attention_mask"),
+                             pixel_values=batch.get("pixel_values"), return_loss=True)
+        loss = outputs["loss"]
+        self.optimizer.zero_grad()
+        loss.backward()
+        if self._world() > 1:
+            self.optimizer.grads_all_reduce(self.process_group)
+        self.optimizer.clip_grad_norm(self.max_grad_norm)
+        lr = self.learning_rate * linear_schedule_with_warmup(step, self.warmup_steps, total_steps)
+        self.optimizer.step(lr=lr)
+        return loss
+
+    def train(self, num_epochs, save_every=1, eval_every=1):
+        total_steps = len(self.train_dataloader) * num_epochs
+        self.total_steps = total_steps
+        best_val_loss = float("inf")
+        step = 0
+        for epoch in range(num_epochs):
+            self.model.train()
+            epoch_loss = 0.0
+            for batch in self.train_dataloader:
+                loss = self.train_step(batch, step, total_steps)
+                step += 1
+                epoch_loss += loss.item()
+            avg_train_loss = epoch_loss / len(self.train_dataloader)
+            print(f"Epoch {epoch + 1} - Average training loss: {avg_train_loss:.4f}")
+            if self.val_dataloader is not None and (epoch + 1) % eval_every == 0:
+                val_loss = self.evaluate()
+                print(f"Epoch {epoch + 1} - Validation loss: {val_loss:.4f}")
+                if val_loss < best_val_loss:
+                    best_val_loss = val_loss
+                    self.save_model(os.path.join(self.output_dir, "best_adapter"))
+            if (epoch + 1) % save_every == 0:
+                self.save_model(os.path.join(self.output_dir, f"adapter_epoch_{epoch + 1}"))
+        self.save_model(os.path.join(self.output_dir, "final_adapter"))
+
+    def evaluate(self):
+        assert self.val_dataloader is not None, "val_dataloader must not be None to run eval"
+        self.model.eval()
+        device = self.model.clip.arena.device
+        val_loss = 0.0
+        with torch.no_grad():
+            for batch in self.val_dataloader:
+                batch = {k: v.to(device) if isinstance(v, torch.Tensor) else v for k, v in batch.items()}
+                outputs = self.model(input_ids=batch.get("input_ids"), attention_mask=batch.get("attention_mask"),
+                                     pixel_values=batch.get("pixel_values"), return_loss=True)
+                val_loss += outputs["loss"].item()
+        return val_loss / len(self.val_dataloader)
+
+    def save_model(self, path):
+        self.model.save_adapter_weights(f"{path}.pt")
+
+    def load_model(self, path):
+        self.model.load_adapter_weights(f"{path}.pt")

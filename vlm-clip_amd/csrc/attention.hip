@@ -1,0 +1,533 @@
+// Fused multi-head attention (head_dim 64) forward/backward for both CLIP towers.
+//
+// Replaces CLIPAttention's core + eager_attention_forward ([HF] modeling_clip.py:259-335):
+// softmax(q k^T * 64^-0.5 + mask) v with the text tower's causal + key-padding mask
+// ([HF] :543-548) and no mask for the vision tower.  q/k/v are read straight out of the
+// fused QKV GEMM output [B*N, 3D] (head h at columns h*64, D+h*64, 2D+h*64); the output O
+// is written [B*N, D] so the out-projection GEMM consumes it directly.  The forward saves
+// the per-row log-sum-exp so the backward recomputes P without storing N x N scores.
+//
+// bf16 path (N <= 256): one workgroup per (batch, head).  K/V (and Q/dO in the backward)
+// live in LDS as [Npad][64] bf16 images with 16-B chunk c of row r stored at c ^ (r & 6);
+// that single swizzle is conflict-free for the ds_read_b128 fragment reads, the
+// ds_read_b64_tr_b16 transposed reads and the 16-B staging writes (tools/lds_banks.py).
+// Scores are computed "key-major" so each lane owns whole query rows: the row max/sum
+// need two xor-shuffles and the P tile feeds the next MFMA straight from registers
+// (cdna_hip_programming.md §3, accumulator as operand, with the k-permutation matched
+// on the V side by the transposed read).  Backward: phase A (dK, dV) has each wave own
+// 16 keys and sweep all queries; phase B (dQ) has each wave own 16 queries and sweep
+// all keys; no atomics, no N x N buffer.
+// f32 path: exact-f32 SIMT kernels (4 lanes per row) for the fp32 parity mode.
+#include "common.h"
+#include "internal.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+__device__ __forceinline__ int img_off(int r, int c) { return r * 128 + ((c ^ (r & 6)) << 4); }
+
+__device__ __forceinline__ bf16x8 frag_row(const char* img, int r, int c) {
+  return *LDS_PTR(const bf16x8, img + img_off(r, c));
+}
+
+// transposed fragment: element j<4 from rows r0+q, j>=4 from rows r0+16+q; column d0 + lane&15
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int r0, int d0, int lane) {
+  const int q = (lane & 15) >> 2;
+  const int col = d0 + 4 * (lane & 3);
+  const int ra = r0 + 4 * (lane >> 4) + q, rb = ra + 16;
+  const int c = col >> 3, h = (col & 7) * 2;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + img_off(ra, c) + h));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + img_off(rb, c) + h));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+
+// stage rows [0, Npad) of a [N][64] head slice (row stride ld elements) into an image
+__device__ __forceinline__ void stage_img(char* img, const bf16* src, int64_t ld, int N, int Npad, int t, int nthr) {
+  for (int id = t; id < Npad * 8; id += nthr) {
+    const int r = id >> 3, c = id & 7;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (r < N) v = *(const u32x4*)(src + (int64_t)r * ld + c * 8);
+    *LDS_PTR(u32x4, img + img_off(r, c)) = v;
+  }
+}
+
+struct AttnP {
+  const bf16* qkv; bf16* o; float* lse; const int64_t* kmask;
+  const bf16* dout; bf16* dqkv;
+  int B, H, N, D;
+  float scale;
+};
+
+// ----------------------------------------------------------------------------- fwd
+template <int NKT, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p) {
+  constexpr int NPAD = NKT * 16;
+  __shared__ __attribute__((aligned(16))) char Kimg[NPAD * 128];
+  __shared__ __attribute__((aligned(16))) char Vimg[NPAD * 128];
+  __shared__ int keyok[NPAD];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int N = p.N, D = p.D;
+  const int64_t ld = 3 * (int64_t)D;
+  const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  stage_img(Kimg, base + D, ld, N, NPAD, t, 256);
+  stage_img(Vimg, base + 2 * D, ld, N, NPAD, t, 256);
+  for (int k = t; k < NPAD; k += 256) keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+  __syncthreads();
+
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const int nqb = (N + 15) >> 4;
+  for (int qb = wave; qb < nqb; qb += 4) {
+    const int q = qb * 16 + li;
+    const int qc = min(q, N - 1);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qf[kk] = *(const bf16x8*)(base + (int64_t)qc * ld + kk * 32 + 8 * g);
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
+    }
+    // s[kt][r] = score(q, key = kt*16 + 4g + r)
+    float mx = NEG_INF;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + 4 * g + r;
+        bool ok = keyok[key] && (!CAUSAL || key <= q);
+        float v = ok ? s[kt][r] * c2 : NEG_INF;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mref = mx == NEG_INF ? 0.f : mx;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float e = exp2f(s[kt][r] - mref);
+        s[kt][r] = e;
+        l += e;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKT / 2; ++ks) {
+      const bf16x8 pf = pack8(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vimg, ks * 32, u * 16, lane), pf, acc[u], 0, 0, 0);
+    }
+    if (q < N) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      bf16* orow = p.o + ((int64_t)b * N + q) * D + h * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[4] = {acc[u][0] * inv, acc[u][1] * inv, acc[u][2] * inv, acc[u][3] * inv};
+        store4(orow + u * 16 + 4 * g, v);
+      }
+      if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? (mref + log2f(l)) * LN2 : NEG_INF;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- bwd
+template <bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int N = p.N, D = p.D;
+  const int NPAD = (N + 31) & ~31;
+  const int64_t ld = 3 * (int64_t)D;
+  char* Qimg = smem;
+  char* Kimg = smem + NPAD * 128;
+  char* Vimg = smem + 2 * NPAD * 128;
+  char* Oimg = smem + 3 * NPAD * 128;  // dO image
+  float* lse2 = (float*)(smem + 4 * NPAD * 128);
+  float* delta = lse2 + NPAD;
+  int* keyok = (int*)(delta + NPAD);
+  const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  const bf16* dob = p.dout + (int64_t)b * N * D + h * 64;
+  stage_img(Qimg, base, ld, N, NPAD, t, 512);
+  stage_img(Kimg, base + D, ld, N, NPAD, t, 512);
+  stage_img(Vimg, base + 2 * D, ld, N, NPAD, t, 512);
+  stage_img(Oimg, dob, D, N, NPAD, t, 512);
+  // delta[q] = sum_d dO*O ; 8 lanes per row
+  {
+    const bf16* ob = p.o + (int64_t)b * N * D + h * 64;
+    for (int id = t; id < NPAD * 8; id += 512) {
+      const int r = id >> 3, c = id & 7;
+      float s = 0.f;
+      if (r < N) {
+        float a[4], bb[4];
+        load4(dob + (int64_t)r * D + c * 8, a);
+        load4(ob + (int64_t)r * D + c * 8, bb);
+        s = a[0] * bb[0] + a[1] * bb[1] + a[2] * bb[2] + a[3] * bb[3];
+        load4(dob + (int64_t)r * D + c * 8 + 4, a);
+        load4(ob + (int64_t)r * D + c * 8 + 4, bb);
+        s += a[0] * bb[0] + a[1] * bb[1] + a[2] * bb[2] + a[3] * bb[3];
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (c == 0) delta[r] = s;
+    }
+  }
+  for (int k = t; k < NPAD; k += 512) {
+    keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+    lse2[k] = k < N ? p.lse[((int64_t)b * p.H + h) * N + k] * LOG2E : __builtin_huge_valf();
+  }
+  __syncthreads();
+
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const int nkb = NPAD >> 4, nstep = NPAD >> 5;
+
+  // ---- phase A: dK, dV for 16 keys per wave
+  for (int kb = wave; kb < nkb; kb += 8) {
+    const int key = kb * 16 + li;  // this lane's key (column of the score tiles)
+    const bool kok = keyok[key];
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kk] = frag_row(Kimg, kb * 16 + li, kk * 4 + g);
+      vf[kk] = frag_row(Vimg, kb * 16 + li, kk * 4 + g);
+    }
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { dv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u] = dv[u]; }
+    for (int qs = 0; qs < nstep; ++qs) {
+      if (CAUSAL && qs * 32 + 31 < kb * 16) continue;  // every query of this step precedes every key
+      f32x4 pt[2], ds[2];
+#pragma unroll
+      for (int tau = 0; tau < 2; ++tau) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = s;
+        const int qr = qs * 32 + tau * 16 + li;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Qimg, qr, kk * 4 + g), kf[kk], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Oimg, qr, kk * 4 + g), vf[kk], dp, 0, 0, 0);
+        }
+        // s[r] = score(q = qs*32 + tau*16 + 4g + r, key)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = qs * 32 + tau * 16 + 4 * g + r;
+          const bool ok = kok && (!CAUSAL || key <= q);
+          const float pv = ok ? exp2f(s[r] * c2 - lse2[q]) : 0.f;
+          pt[tau][r] = pv;
+          ds[tau][r] = pv * (dp[r] - delta[q]);
+        }
+      }
+      const bf16x8 pf = pack8(pt[0], pt[1]);
+      const bf16x8 sf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Oimg, qs * 32, u * 16, lane), pf, dv[u], 0, 0, 0);
+        dk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Qimg, qs * 32, u * 16, lane), sf, dk[u], 0, 0, 0);
+      }
+    }
+    if (key < N) {
+      bf16* row = p.dqkv + ((int64_t)b * N + key) * ld + h * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float a[4] = {dk[u][0] * p.scale, dk[u][1] * p.scale, dk[u][2] * p.scale, dk[u][3] * p.scale};
+        float c[4] = {dv[u][0], dv[u][1], dv[u][2], dv[u][3]};
+        store4(row + D + u * 16 + 4 * g, a);
+        store4(row + 2 * D + u * 16 + 4 * g, c);
+      }
+    }
+  }
+
+  // ---- phase B: dQ for 16 queries per wave
+  const int nqb = (N + 15) >> 4;
+  for (int qb = wave; qb < nqb; qb += 8) {
+    const int q = qb * 16 + li;
+    const float l2 = lse2[q], dl = delta[q];
+    bf16x8 qf[2], of[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[kk] = frag_row(Qimg, q, kk * 4 + g);
+      of[kk] = frag_row(Oimg, q, kk * 4 + g);
+    }
+    f32x4 dq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dq[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nstep; ++ks) {
+      if (CAUSAL && ks * 32 > qb * 16 + 15) break;
+      f32x4 ds[2];
+#pragma unroll
+      for (int tau = 0; tau < 2; ++tau) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = s;
+        const int kr = ks * 32 + tau * 16 + li;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kr, kk * 4 + g), qf[kk], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Vimg, kr, kk * 4 + g), of[kk], dp, 0, 0, 0);
+        }
+        // s[r] = score(q, key = ks*32 + tau*16 + 4g + r)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = ks * 32 + tau * 16 + 4 * g + r;
+          const bool ok = keyok[key] && (!CAUSAL || key <= q);
+          const float pv = ok ? exp2f(s[r] * c2 - l2) : 0.f;
+          ds[tau][r] = pv * (dp[r] - dl);
+        }
+      }
+      const bf16x8 sf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        dq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Kimg, ks * 32, u * 16, lane), sf, dq[u], 0, 0, 0);
+    }
+    if (q < N) {
+      bf16* row = p.dqkv + ((int64_t)b * N + q) * ld + h * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float a[4] = {dq[u][0] * p.scale, dq[u][1] * p.scale, dq[u][2] * p.scale, dq[u][3] * p.scale};
+        store4(row + u * 16 + 4 * g, a);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ f32 SIMT path
+// 4 lanes per row, 16 head dims each.  K/V (or Q/dO) staged in LDS as fp32 [N][64].
+struct AttnF {
+  const float* qkv; float* o; float* lse; const int64_t* kmask;
+  const float* dout; float* dqkv;
+  int B, H, N, D, causal;
+  float scale;
+};
+
+__device__ __forceinline__ float dot16(const float* a, const float* b) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s = fmaf(a[i], b[i], s);
+  return s;
+}
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(1024) void attn_fwd_f32(AttnF p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Ks = (float*)smem;
+  float* Vs = Ks + p.N * 64;
+  int* ok = (int*)(Vs + p.N * 64);
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H, N = p.N, D = p.D;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
+    const int r = i >> 6, c = i & 63;
+    Ks[i] = base[(int64_t)r * ld + D + c];
+    Vs[i] = base[(int64_t)r * ld + 2 * D + c];
+  }
+  for (int k = threadIdx.x; k < N; k += blockDim.x) ok[k] = !p.kmask || p.kmask[(int64_t)b * N + k] != 0;
+  __syncthreads();
+  const int sub = threadIdx.x & 3;
+  for (int q = threadIdx.x >> 2; q < N; q += blockDim.x >> 2) {  // the 4 lanes of a row share q
+    float qv[16], acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { qv[i] = base[(int64_t)q * ld + sub * 16 + i] * p.scale; acc[i] = 0.f; }
+    float m = NEG_INF, l = 0.f;
+    const int kend = p.causal ? q + 1 : N;
+    for (int k = 0; k < kend; ++k) {
+      if (!ok[k]) continue;
+      const float s = quad_sum(dot16(qv, Ks + k * 64 + sub * 16));
+      const float mn = fmaxf(m, s);
+      const float corr = expf(m - mn), e = expf(s - mn);
+      l = l * corr + e;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = acc[i] * corr + e * Vs[k * 64 + sub * 16 + i];
+      m = mn;
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    float* orow = p.o + ((int64_t)b * N + q) * D + h * 64 + sub * 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) orow[i] = acc[i] * inv;
+    if (sub == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? m + logf(l) : NEG_INF;
+  }
+}
+
+__global__ __launch_bounds__(1024) void attn_bwd_f32(AttnF p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* A = (float*)smem;          // phase 1: K, phase 2: Q
+  float* Bm = A + p.N * 64;         // phase 1: V, phase 2: dO
+  float* lse = Bm + p.N * 64;
+  float* dlt = lse + p.N;
+  int* ok = (int*)(dlt + p.N);
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H, N = p.N, D = p.D;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  const float* dob = p.dout + (int64_t)b * N * D + h * 64;
+  const float* ob = p.o + (int64_t)b * N * D + h * 64;
+  float* dq_base = p.dqkv + (int64_t)b * N * ld + h * 64;
+  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
+    const int r = i >> 6, c = i & 63;
+    A[i] = base[(int64_t)r * ld + D + c];
+    Bm[i] = base[(int64_t)r * ld + 2 * D + c];
+  }
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    ok[k] = !p.kmask || p.kmask[(int64_t)b * N + k] != 0;
+    lse[k] = p.lse[((int64_t)b * p.H + h) * N + k];
+    float s = 0.f;
+    for (int c = 0; c < 64; ++c) s += dob[(int64_t)k * D + c] * ob[(int64_t)k * D + c];
+    dlt[k] = s;
+  }
+  __syncthreads();
+  const int sub = threadIdx.x & 3;
+  // phase 1: dQ rows
+  for (int q = threadIdx.x >> 2; q < N; q += blockDim.x >> 2) {
+    float qv[16], dov[16], dq[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      qv[i] = base[(int64_t)q * ld + sub * 16 + i];
+      dov[i] = dob[(int64_t)q * D + sub * 16 + i];
+      dq[i] = 0.f;
+    }
+    const int kend = p.causal ? q + 1 : N;
+    for (int k = 0; k < kend; ++k) {
+      if (!ok[k]) continue;
+      const float s = quad_sum(dot16(qv, A + k * 64 + sub * 16)) * p.scale;
+      const float pr = expf(s - lse[q]);
+      const float dp = quad_sum(dot16(dov, Bm + k * 64 + sub * 16));
+      const float ds = pr * (dp - dlt[q]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dq[i] = fmaf(ds, A[k * 64 + sub * 16 + i], dq[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq_base[(int64_t)q * ld + sub * 16 + i] = dq[i] * p.scale;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
+    const int r = i >> 6, c = i & 63;
+    A[i] = base[(int64_t)r * ld + c];
+    Bm[i] = dob[(int64_t)r * D + c];
+  }
+  __syncthreads();
+  // phase 2: dK, dV rows
+  for (int k = threadIdx.x >> 2; k < N; k += blockDim.x >> 2) {
+    float kv[16], vv[16], dk[16], dv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      kv[i] = base[(int64_t)k * ld + D + sub * 16 + i];
+      vv[i] = base[(int64_t)k * ld + 2 * D + sub * 16 + i];
+      dk[i] = 0.f; dv[i] = 0.f;
+    }
+    const bool kok = ok[k];
+    for (int q = p.causal ? k : 0; q < N && kok; ++q) {
+      const float s = quad_sum(dot16(kv, A + q * 64 + sub * 16)) * p.scale;
+      const float pr = expf(s - lse[q]);
+      const float dp = quad_sum(dot16(vv, Bm + q * 64 + sub * 16));
+      const float ds = pr * (dp - dlt[q]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dv[i] = fmaf(pr, Bm[q * 64 + sub * 16 + i], dv[i]);
+        dk[i] = fmaf(ds, A[q * 64 + sub * 16 + i], dk[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dq_base[(int64_t)k * ld + D + sub * 16 + i] = dk[i] * p.scale;
+      dq_base[(int64_t)k * ld + 2 * D + sub * 16 + i] = dv[i];
+    }
+  }
+}
+
+template <bool C>
+int fwd_dispatch(const AttnP& p, hipStream_t s) {
+  const int nkt = ((p.N + 31) & ~31) / 16;
+  const dim3 g(p.B * p.H), blk(256);
+  switch (nkt) {
+    case 2: hipLaunchKernelGGL((attn_fwd_mfma<2, C>), g, blk, 0, s, p); break;
+    case 4: hipLaunchKernelGGL((attn_fwd_mfma<4, C>), g, blk, 0, s, p); break;
+    case 6: hipLaunchKernelGGL((attn_fwd_mfma<6, C>), g, blk, 0, s, p); break;
+    case 8: hipLaunchKernelGGL((attn_fwd_mfma<8, C>), g, blk, 0, s, p); break;
+    case 10: hipLaunchKernelGGL((attn_fwd_mfma<10, C>), g, blk, 0, s, p); break;
+    case 12: hipLaunchKernelGGL((attn_fwd_mfma<12, C>), g, blk, 0, s, p); break;
+    case 14: hipLaunchKernelGGL((attn_fwd_mfma<14, C>), g, blk, 0, s, p); break;
+    case 16: hipLaunchKernelGGL((attn_fwd_mfma<16, C>), g, blk, 0, s, p); break;
+    default: return clipmi_invalid("attention: N must be <= 256");
+  }
+  return CLIPMI_OK;
+}
+
+}  // namespace
+
+// attention_mask: int64 [B, N] key-padding mask (1 = keep) or NULL; causal: text tower.
+extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse,
+                                    const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
+  CLIPMI_REQUIRE(N >= 1 && N <= 256, "N must be in [1, 256]");
+  if (B == 0) return CLIPMI_OK;
+  if (dtype == CLIPMI_BF16) {
+    AttnP p{(const bf16*)qkv, (bf16*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
+    CLIPMI_TRY(causal ? fwd_dispatch<true>(p, s) : fwd_dispatch<false>(p, s));
+  } else {
+    AttnF p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, causal, 0.125f};
+    size_t lds = (size_t)N * 64 * 4 * 2 + N * 4;
+    static bool attr = false;
+    if (!attr) {
+      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_fwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(attn_fwd_f32, dim3(B * H), dim3(1024), lds, s, p);
+  }
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, const void* o, const float* lse,
+                                    const void* dout, void* dqkv, const int64_t* attention_mask, int causal,
+                                    int B, int H, int N, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
+  CLIPMI_REQUIRE(N >= 1 && N <= 256, "N must be in [1, 256]");
+  if (B == 0) return CLIPMI_OK;
+  if (dtype == CLIPMI_BF16) {
+    AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
+    const int npad = (N + 31) & ~31;
+    size_t lds = (size_t)npad * 128 * 4 + (size_t)npad * 12;
+    static bool attr = false;
+    if (!attr) {
+      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    if (causal) hipLaunchKernelGGL(attn_bwd_mfma<true>, dim3(B * H), dim3(512), lds, s, p);
+    else hipLaunchKernelGGL(attn_bwd_mfma<false>, dim3(B * H), dim3(512), lds, s, p);
+  } else {
+    AttnF p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D, causal, 0.125f};
+    size_t lds = (size_t)N * 64 * 4 * 2 + N * 12;
+    static bool attr = false;
+    if (!attr) {
+      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(attn_bwd_f32, dim3(B * H), dim3(1024), lds, s, p);
+  }
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}

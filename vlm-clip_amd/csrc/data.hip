@@ -1,0 +1,103 @@
+// Data-movement kernels around the towers: patch im2col and pooled-row gather/scatter.
+//
+// im2col replaces the stride=kernel Conv2d of CLIPVisionEmbeddings ([HF] modeling_clip.py
+// :148-154, :211-212) as a coalesced gather feeding the MFMA GEMM; its output has one zero
+// row per image in the CLS slot, so the patch GEMM writes the full [B*(Np+1), D] token
+// matrix in place and the patch-weight gradient is one wgrad GEMM over that same buffer.
+// Pooling: model_m.py:102,122 take token 0 ([:,0,:]); HF's EOS pooler ([HF] :561-581)
+// takes the first EOS (or argmax id when eos_token_id == 2).
+#include "common.h"
+#include "internal.h"
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_kernel(const float* px, T* X, int B, int C, int Hh, int P, int G,
+                                                     int K, int Kp) {
+  const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  const int Np1 = G * G + 1;
+  if (row >= (int64_t)B * Np1) return;
+  const int b = (int)(row / Np1), t = (int)(row % Np1);
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < Kp; k += gridDim.x * 256) {
+    float v = 0.f;
+    if (t > 0 && k < K) {
+      const int p = t - 1, gy = p / G, gx = p % G;
+      const int c = k / (P * P), r = k % (P * P), ky = r / P, kx = r % P;
+      v = px[(((int64_t)b * C + c) * Hh + gy * P + ky) * Hh + gx * P + kx];
+    }
+    X[row * Kp + k] = (T)v;
+  }
+}
+
+// idx[b] = pooled token: mode 0 -> 0, mode 1 -> first position with id == eos, mode 2 -> argmax id
+__global__ void pool_index_kernel(const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int best = 0;
+  if (mode == 1) {
+    for (int s = S - 1; s >= 0; --s)
+      if (ids[(int64_t)b * S + s] == eos) best = s;
+  } else if (mode == 2) {
+    int64_t bv = ids[(int64_t)b * S];
+    for (int s = 1; s < S; ++s)
+      if (ids[(int64_t)b * S + s] > bv) { bv = ids[(int64_t)b * S + s]; best = s; }
+  }
+  idx[b] = best;
+}
+
+// out[b][:] = src[(b*S + idx[b])][:]  (idx == NULL -> token 0)
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const T* src, const int* idx, int B, int S, int D, T* out) {
+  const int b = blockIdx.x;
+  const int64_t r = (int64_t)b * S + (idx ? idx[b] : 0);
+  for (int c = threadIdx.x; c < D; c += 256) out[(int64_t)b * D + c] = src[r * D + c];
+}
+
+// dst[(b*S + idx[b])][:] (+)= src[b][:]
+template <typename T>
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const T* src, const int* idx, int B, int S, int D, T* dst,
+                                                           int beta) {
+  const int b = blockIdx.x;
+  const int64_t r = (int64_t)b * S + (idx ? idx[b] : 0);
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float v = (float)src[(int64_t)b * D + c];
+    if (beta) v += (float)dst[r * D + c];
+    dst[r * D + c] = (T)v;
+  }
+}
+
+}  // namespace
+
+extern "C" int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, int C, int H, int P, int Kp) {
+  CLIPMI_REQUIRE(H % P == 0, "image size must be a multiple of the patch size");
+  const int G = H / P, K = C * P * P;
+  CLIPMI_REQUIRE(Kp >= K && Kp % 8 == 0, "Kp must be >= C*P*P and a multiple of 8");
+  const int64_t rows = (int64_t)B * (G * G + 1);
+  if (rows == 0) return CLIPMI_OK;
+  dim3 g((Kp + 255) / 256 > 4 ? 4 : (Kp + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535),
+         (unsigned)((rows + 65534) / 65535));
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(im2col_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, pixels, (bf16*)X, B, C, H, P, G, K, Kp);
+  else hipLaunchKernelGGL(im2col_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, pixels, (float*)X, B, C, H, P, G, K, Kp);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_pool_index(void* stream, const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx) {
+  hipLaunchKernelGGL(pool_index_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, ids, B, S, eos, mode, idx);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* out) {
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(gather_rows_kernel<bf16>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, idx, B, S, D, (bf16*)out);
+  else hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const float*)src, idx, B, S, D, (float*)out);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* dst, int beta) {
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(scatter_rows_kernel<bf16>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, idx, B, S, D, (bf16*)dst, beta);
+  else hipLaunchKernelGGL(scatter_rows_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const float*)src, idx, B, S, D, (float*)dst, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}

@@ -1,0 +1,183 @@
+// Native encoder engine: sequences a whole CLIPEncoder (L pre-LN layers) forward and
+// backward on one HIP stream with one C-ABI call per direction.
+//
+// Replaces CLIPEncoder.forward ([HF] modeling_clip.py:477-482) and, through autograd in
+// the reference, its backward.  Per layer ([HF] :362-383):
+//   ln1 = LN1(x)                      -> clipmi_layernorm_fwd
+//   qkv = ln1 Wqkv^T + bqkv           -> GEMM (q/k/v fused into one [3D, D] weight)
+//   o   = attention(qkv)              -> clipmi_attention_fwd
+//   h   = x + o Wo^T + bo             -> GEMM, residual fused in the epilogue
+//   ln2 = LN2(h)
+//   a   = quick_gelu(ln2 W1^T + b1)   -> GEMM, bias+activation fused, pre-activation saved
+//   y   = h + a W2^T + b2             -> GEMM, residual fused
+// Backward mirrors it with dgrad GEMMs (activation derivative fused in the epilogue),
+// split-K wgrad GEMMs accumulating straight into the fp32 gradient arena, deterministic
+// column sums for biases, and LN backward with the residual gradient fused.
+// Activation buffers are caller-owned (per layer for training; one shared set for
+// inference), so the engine holds no state and allocates nothing.
+#include <algorithm>
+#include <cstring>
+#include "internal.h"
+
+extern "C" {
+int clipmi_layernorm_fwd(void*, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int, int,
+                         float, const void*, const void*, int);
+int64_t clipmi_layernorm_bwd_ws(int R, int D);
+int clipmi_layernorm_bwd(void*, int, const void*, int64_t, const void*, int64_t, const float*, const float*, const void*,
+                         void*, int64_t, const void*, int64_t, float*, float*, int, void*, int64_t, int, int);
+int64_t clipmi_colsum_ws(int R, int N);
+int clipmi_colsum(void*, int, const void*, int64_t, int, int, float*, int, void*, int64_t);
+int clipmi_attention_fwd(void*, int, const void*, void*, float*, const int64_t*, int, int, int, int, int);
+int clipmi_attention_bwd(void*, int, const void*, const void*, const float*, const void*, void*, const int64_t*, int,
+                         int, int, int, int);
+}
+
+namespace {
+
+size_t esize(int dt) { return dt == CLIPMI_BF16 ? 2 : 4; }
+int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb,
+         bool bkm, void* C, int64_t ldc, int c_dt, int flags, const void* bias = nullptr, const void* res = nullptr,
+         int64_t ldr = 0, void* aux = nullptr, int64_t ldaux = 0, int split = 1, void* ws = nullptr,
+         int64_t ws_bytes = 0) {
+  clipmi_gemm_desc d;
+  memset(&d, 0, sizeof(d));
+  d.M = M; d.N = N; d.K = K;
+  d.A = A; d.lda = lda; d.a_kmajor = akm;
+  d.B = B; d.ldb = ldb; d.b_kmajor = bkm;
+  d.C = C; d.ldc = ldc;
+  d.bias = bias; d.residual = res; d.ldr = ldr; d.aux = aux; d.ldaux = ldaux;
+  d.alpha = 1.f; d.flags = flags;
+  d.ab_dtype = dt; d.c_dtype = c_dt; d.bias_dtype = dt;
+  d.split_k = split; d.workspace = ws; d.workspace_bytes = ws_bytes;
+  return clipmi_gemm(s, &d);
+}
+
+// split-K factor for a wgrad GEMM [M x N] reducing over K tokens
+int wgrad_splits(int M, int N, int K, int dt) {
+  const int tile = dt == CLIPMI_BF16 ? 128 : 64;
+  const int tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
+  int s = std::max(1, 1024 / std::max(1, tiles));
+  s = std::min(s, 32);
+  while (s > 1 && (int64_t)K / s < 512) --s;
+  return s;
+}
+
+struct WsPlan {
+  int64_t g2, dln, dbig, split, colsum, ln, total;
+};
+
+WsPlan plan(const clipmi_encoder_desc* d) {
+  const int64_t R = (int64_t)d->B * d->N;
+  const size_t es = esize(d->dtype);
+  WsPlan p;
+  const int64_t big = std::max<int64_t>(3 * d->D, d->F);
+  p.g2 = 0;
+  p.dln = p.g2 + align256(R * d->D * es);
+  p.dbig = p.dln + align256(R * d->D * es);
+  p.split = p.dbig + align256(R * big * es);
+  int64_t sp = 0;
+  const int shapes[4][2] = {{d->F, d->D}, {d->D, d->F}, {d->D, d->D}, {3 * d->D, d->D}};
+  for (auto& sh : shapes) {
+    const int s = wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
+    if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * sh[1] * 4);
+  }
+  p.colsum = p.split + align256(sp);
+  p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));
+  p.total = p.ln + align256(clipmi_layernorm_bwd_ws((int)R, d->D));
+  return p;
+}
+
+int validate(const clipmi_encoder_desc* d) {
+  CLIPMI_REQUIRE(d && d->layers && d->act, "null descriptor");
+  CLIPMI_REQUIRE(d->dtype == CLIPMI_BF16 || d->dtype == CLIPMI_F32, "dtype");
+  CLIPMI_REQUIRE(d->D == d->H * 64, "hidden size must be heads * 64");
+  CLIPMI_REQUIRE(d->B >= 0 && d->N >= 1 && d->L >= 1, "shape");
+  return CLIPMI_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d) { return plan(d).total; }
+
+extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
+  CLIPMI_TRY(validate(d));
+  const int dt = d->dtype;
+  const int R = d->B * d->N, D = d->D, F = d->F;
+  if (R == 0) return CLIPMI_OK;
+  for (int l = 0; l < d->L; ++l) {
+    const clipmi_layer_w& w = d->layers[l];
+    const clipmi_layer_act& a = d->act[l];
+    void* x_out = (l + 1 < d->L) ? d->act[l + 1].x_in : d->x_out;
+    CLIPMI_TRY(clipmi_layernorm_fwd(s, dt, a.x_in, D, a.ln1, D, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps,
+                                    nullptr, nullptr, 0));
+    CLIPMI_TRY(gemm(s, dt, R, 3 * D, D, a.ln1, D, true, w.qkv_w, D, true, a.qkv, 3 * D, dt, CLIPMI_EPI_BIAS, w.qkv_b));
+    CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    CLIPMI_TRY(gemm(s, dt, R, D, D, a.o, D, true, w.out_w, D, true, a.h, D, dt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
+                    w.out_b, a.x_in, D));
+    CLIPMI_TRY(clipmi_layernorm_fwd(s, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
+                                    nullptr, nullptr, 0));
+    const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_PRE : 0);
+    CLIPMI_TRY(gemm(s, dt, R, F, D, a.ln2, D, true, w.fc1_w, D, true, a.act, F, dt, f1, w.fc1_b, nullptr, 0, a.pre, F));
+    CLIPMI_TRY(gemm(s, dt, R, D, F, a.act, F, true, w.fc2_w, F, true, x_out, D, dt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
+                    w.fc2_b, a.h, D));
+  }
+  return CLIPMI_OK;
+}
+
+// dx: gradient w.r.t. the encoder output on entry; overwritten with the gradient w.r.t.
+// the encoder input (layer 0's x_in) on exit.  Grads accumulate into d->grads (fp32).
+extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* dx) {
+  CLIPMI_TRY(validate(d));
+  CLIPMI_REQUIRE(d->grads, "encoder_bwd needs gradient destinations");
+  const int dt = d->dtype;
+  const int R = d->B * d->N, D = d->D, F = d->F;
+  if (R == 0) return CLIPMI_OK;
+  const WsPlan p = plan(d);
+  CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= p.total, "encoder_bwd workspace too small");
+  char* ws = (char*)d->workspace;
+  void* g2 = ws + p.g2;
+  void* dln = ws + p.dln;
+  void* dbig = ws + p.dbig;
+  void* wsplit = ws + p.split;
+  void* wcol = ws + p.colsum;
+  void* wln = ws + p.ln;
+  const int64_t split_bytes = p.colsum - p.split;
+  const int64_t col_bytes = p.ln - p.colsum;
+  const int64_t ln_bytes = p.total - p.ln;
+  const int f32 = CLIPMI_F32;
+  auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C) {
+    const int sp = wgrad_splits(M, N, R, dt);
+    return gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
+                nullptr, 0, sp, wsplit, split_bytes);
+  };
+  for (int l = d->L - 1; l >= 0; --l) {
+    const clipmi_layer_w& w = d->layers[l];
+    const clipmi_layer_act& a = d->act[l];
+    const clipmi_layer_grad& g = d->grads[l];
+    CLIPMI_REQUIRE(a.pre, "training forward must save pre-activations");
+    // MLP branch: dx is dL/dy
+    CLIPMI_TRY(gemm(s, dt, R, F, D, dx, D, true, w.fc2_w, F, false, dbig, F, dt, CLIPMI_EPI_DQGELU, nullptr, nullptr,
+                    0, a.pre, F));                                          // d_pre = (dx W2) * qgelu'(pre)
+    CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w));                     // gW2 += dx^T act
+    CLIPMI_TRY(clipmi_colsum(s, dt, dx, D, R, D, g.fc2_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w));                   // gW1 += d_pre^T ln2
+    CLIPMI_TRY(clipmi_colsum(s, dt, dbig, F, R, F, g.fc1_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(gemm(s, dt, R, D, F, dbig, F, true, w.fc1_w, D, false, dln, D, dt, 0));  // d_ln2 = d_pre W1
+    CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx, D, g.ln2_w, g.ln2_b,
+                                    1, wln, ln_bytes, R, D));              // dh = dx + LN2'(d_ln2)
+    // attention branch: g2 is dL/dh
+    CLIPMI_TRY(gemm(s, dt, R, D, D, g2, D, true, w.out_w, D, false, dln, D, dt, 0));     // d_o = dh Wo
+    CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w));                                     // gWo += dh^T o
+    CLIPMI_TRY(clipmi_colsum(s, dt, g2, D, R, D, g.out_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                    d->N, D));                              // d_qkv
+    CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w));           // gWqkv += d_qkv^T ln1
+    CLIPMI_TRY(clipmi_colsum(s, dt, dbig, 3 * D, R, 3 * D, g.qkv_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
+    CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
+                                    g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
+  }
+  return CLIPMI_OK;
+}

@@ -25,6 +25,7 @@
 // f32 path: exact-f32 LDS-tiled SIMT kernel with the same epilogue (parity mode).
 #include "common.h"
 #include "internal.h"
+#include <algorithm>
 
 namespace {
 
@@ -40,23 +41,41 @@ struct GemmP {
   float alpha; int flags; int bias_f32;
   int k_per_split; float* ws;
   int tiles_n, ntiles;
+  int vec;  // all leading dimensions multiples of 4 elements
 };
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
   return p.bias_f32 ? ((const float*)p.bias)[n] : (float)((const bf16*)p.bias)[n];
 }
 
-// v holds C[m][n..n+3] before the epilogue.
+// v holds C[m][n..n+3] before the epilogue; columns >= N are dropped.  Vector loads and
+// stores when the 4 columns are in range and every leading dimension keeps them aligned.
+template <typename OutT>
+__device__ __forceinline__ void ld4(const OutT* p, float v[4], int nv, bool vec) {
+  if (vec) { load4(p, v); return; }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = j < nv ? to_f32(p[j]) : 0.f;
+}
+template <typename OutT>
+__device__ __forceinline__ void st4(OutT* p, const float v[4], int nv, bool vec) {
+  if (vec) { store4(p, v); return; }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < nv) p[j] = from_f32<OutT>(v[j]);
+}
+
 template <typename OutT>
 __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[4]) {
   const int f = p.flags;
+  const int nv = min(4, p.N - n);
+  const bool vec = p.vec && nv == 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] *= p.alpha;
   if (f & CLIPMI_EPI_BIAS) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += ld_bias(p, n + j);
+    for (int j = 0; j < 4; ++j) v[j] += j < nv ? ld_bias(p, n + j) : 0.f;
   }
-  if (f & CLIPMI_EPI_STORE_PRE) store4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v);
+  if (f & CLIPMI_EPI_STORE_PRE) st4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v, nv, vec);
   if (f & CLIPMI_EPI_QGELU) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
@@ -66,7 +85,7 @@ __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[
   }
   if (f & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)) {
     float a[4];
-    load4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, a);
+    ld4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, a, nv, vec);
     if (f & CLIPMI_EPI_DQGELU) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] *= quick_gelu_grad(a[j]);
@@ -77,18 +96,18 @@ __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[
   }
   if (f & CLIPMI_EPI_RESID) {
     float r[4];
-    load4((const OutT*)p.res + (int64_t)m * p.ldr + n, r);
+    ld4((const OutT*)p.res + (int64_t)m * p.ldr + n, r, nv, vec);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] += r[j];
   }
   OutT* c = (OutT*)p.C + (int64_t)m * p.ldc + n;
   if (f & CLIPMI_EPI_BETA) {
     float o[4];
-    load4(c, o);
+    ld4(c, o, nv, vec);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] += o[j];
   }
-  store4(c, v);
+  st4(c, v, nv, vec);
 }
 
 // ---------------------------------------------------------------- LDS images
@@ -235,7 +254,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
       if (n >= p.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (p.ws) {
-        store4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v);
+        st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
       } else {
         epilogue4<OutT>(p, m, n, v);
       }
@@ -294,7 +313,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p, int akm, int bkm
     int m = m0 + ty * 4 + i, n = n0 + tx * 4;
     if (m >= p.M || n >= p.N) continue;
     float v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
-    if (p.ws) store4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v);
+    if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
     else epilogue4<OutT>(p, m, n, v);
   }
 }
@@ -302,16 +321,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p, int akm, int bkm
 // split-K reduction: C (fp32) = [C +] alpha * sum_z ws[z]
 __global__ void splitk_reduce_kernel(const float* ws, float* C, int64_t ldc, int M, int N, int splits,
                                      float alpha, int beta) {
-  int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  int64_t total = (int64_t)M * N;
-  if (i4 >= total) return;
-  int m = (int)(i4 / N), n = (int)(i4 - (int64_t)m * N);
-  f32x4 s = *(const f32x4*)(ws + i4);
-  for (int z = 1; z < splits; ++z) s += *(const f32x4*)(ws + (int64_t)z * total + i4);
-  float* c = C + (int64_t)m * ldc + n;
-  f32x4 o = s * alpha;
-  if (beta) o += *(const f32x4*)c;
-  *(f32x4*)c = o;
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+    float sum = 0.f;
+    for (int z = 0; z < splits; ++z) sum += ws[(int64_t)z * total + i];
+    float* c = C + (int64_t)m * ldc + n;
+    *c = beta ? *c + alpha * sum : alpha * sum;
+  }
 }
 
 template <bool AK, bool BKM, typename OutT>
@@ -324,11 +341,12 @@ void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
-  if (d->M == 0 || d->N == 0) return CLIPMI_OK;
-  CLIPMI_REQUIRE(d->N % 8 == 0, "N must be a multiple of 8");
-  CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32 || d->c_dtype == CLIPMI_BF16, "c_dtype");
   const bool bf = d->ab_dtype == CLIPMI_BF16;
   CLIPMI_REQUIRE(bf || d->ab_dtype == CLIPMI_F32, "ab_dtype");
+  if (d->M == 0 || d->N == 0) return CLIPMI_OK;
+  CLIPMI_REQUIRE(bf == false || d->b_kmajor || d->N % 8 == 0, "row-major B needs N % 8 == 0");
+  CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32 || d->c_dtype == CLIPMI_BF16, "c_dtype");
+
   if (bf) {
     CLIPMI_REQUIRE(!d->a_kmajor || d->K % 8 == 0, "k-major A needs K % 8 == 0");
     CLIPMI_REQUIRE(!d->b_kmajor || d->K % 8 == 0, "k-major B needs K % 8 == 0");
@@ -337,7 +355,6 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     CLIPMI_REQUIRE(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0, "A/B must be 16-byte aligned");
     CLIPMI_REQUIRE((d->lda % 8) == 0 && (d->ldb % 8) == 0, "lda/ldb must be multiples of 8");
   }
-  CLIPMI_REQUIRE((d->ldc % 4) == 0, "ldc must be a multiple of 4");
   int splits = d->split_k > 1 ? d->split_k : 1;
   GemmP p;
   p.M = d->M; p.N = d->N; p.K = d->K;
@@ -346,6 +363,8 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
   p.bias_f32 = d->bias_dtype == CLIPMI_F32;
   p.ws = nullptr;
+  p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
+          ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
   const int tile = bf ? BM : FT;
   const int kstep = bf ? BK : FK;
   if (splits > 1) {
@@ -388,10 +407,9 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }
   CLIPMI_CHECK_LAUNCH();
   if (p.ws) {
-    int64_t total4 = ((int64_t)d->M * d->N) / 4;
-    CLIPMI_REQUIRE(((int64_t)d->M * d->N) % 4 == 0, "M*N % 4");
-    CLIPMI_REQUIRE(d->ldc == d->N || d->M == 1 || true, "");
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s,
+    const int64_t total = (int64_t)d->M * d->N;
+    const unsigned nblk = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
                        p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha,
                        (d->flags & CLIPMI_EPI_BETA) ? 1 : 0);
     CLIPMI_CHECK_LAUNCH();

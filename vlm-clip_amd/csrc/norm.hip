@@ -1,0 +1,447 @@
+// LayerNorm forward/backward, column reductions (bias / LN-affine / position grads) and
+// the embedding gathers/scatters of both towers.
+//
+// Replaces: nn.LayerNorm in [HF] modeling_clip.py:357,359 (layer_norm1/2), :605,642
+// (pre_layrnorm), :559 (final_layer_norm), adapter/clip_adapter.py:15,142 (adapter LN);
+// CLIPVisionEmbeddings.forward [HF] :202-219 (CLS concat + position add, fused into the
+// pre-LN here); CLIPTextEmbeddings.forward [HF] :232-256 (token + position gather).
+//
+// One wave per row; a lane holds NP pieces of PS contiguous elements at element offset
+// (k*64 + lane)*PS, so every load instruction is fully coalesced.  Statistics in fp32,
+// two-pass variance from registers (no E[x^2]-E[x]^2 cancellation).
+#include "common.h"
+#include "internal.h"
+
+namespace {
+
+template <typename T, int PS> struct Vec;
+template <> struct Vec<float, 4> { typedef f32x4 type; };
+template <> struct Vec<float, 2> { typedef __attribute__((ext_vector_type(2))) float type; };
+template <> struct Vec<float, 1> { typedef float type; };
+template <> struct Vec<bf16, 4> { typedef bf16x4 type; };
+template <> struct Vec<bf16, 2> { typedef bf16x2 type; };
+template <> struct Vec<bf16, 1> { typedef bf16 type; };
+
+template <typename T, int PS>
+__device__ __forceinline__ void vload(const T* p, float* o) {
+  typename Vec<T, PS>::type v = *(const typename Vec<T, PS>::type*)p;
+  if constexpr (PS == 1) { o[0] = (float)v; }
+  else {
+#pragma unroll
+    for (int j = 0; j < PS; ++j) o[j] = (float)v[j];
+  }
+}
+template <typename T, int PS>
+__device__ __forceinline__ void vstore(T* p, const float* o) {
+  typename Vec<T, PS>::type v;
+  if constexpr (PS == 1) { v = (T)o[0]; }
+  else {
+#pragma unroll
+    for (int j = 0; j < PS; ++j) v[j] = (T)o[j];
+  }
+  *(typename Vec<T, PS>::type*)p = v;
+}
+
+// y = LN(x [+ pos[row % period] + (row % period == 0 ? cls : 0)]) * w + b
+// When pos is given the pre-LN sum is written back to x (the vision embedding output).
+template <typename T, int PS, int NP>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
+                                                     float* mean_out, float* rstd_out, int R, int D, float eps,
+                                                     const T* pos, const T* cls, int period) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  T* xr = x + (int64_t)row * ldx;
+  float v[NP][PS];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = (k * 64 + lane) * PS;
+    vload<T, PS>(xr + c, v[k]);
+    if (pos) {
+      const int t = row % period;
+      float pv[PS];
+      vload<T, PS>(pos + (int64_t)t * D + c, pv);
+#pragma unroll
+      for (int j = 0; j < PS; ++j) v[k][j] += pv[j];
+      if (cls && t == 0) {
+        vload<T, PS>(cls + c, pv);
+#pragma unroll
+        for (int j = 0; j < PS; ++j) v[k][j] += pv[j];
+      }
+      vstore<T, PS>(xr + c, v[k]);
+    }
+#pragma unroll
+    for (int j = 0; j < PS; ++j) s += v[k][j];
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+#pragma unroll
+    for (int j = 0; j < PS; ++j) { float d = v[k][j] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  T* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = (k * 64 + lane) * PS;
+    float wv[PS], bv[PS], o[PS];
+    vload<T, PS>(w + c, wv);
+    vload<T, PS>(b + c, bv);
+#pragma unroll
+    for (int j = 0; j < PS; ++j) o[j] = (v[k][j] - mean) * rstd * wv[j] + bv[j];
+    vstore<T, PS>(yr + c, o);
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// dx = [dres +] rstd * (g - mean(g) - xhat * mean(g*xhat)),  g = dy * w
+// per-block partial dgamma/dbeta -> ws[blockIdx][2][D]
+template <typename T, int PS, int NP>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, const T* x, int64_t ldx,
+                                                     const float* mean, const float* rstd, const T* w,
+                                                     T* dx, int64_t lddx, const T* dres, int64_t ldres,
+                                                     float* ws, int R, int D) {
+  __shared__ float red[4][2][NP * PS * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[NP][PS], pb[NP][PS];
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+#pragma unroll
+    for (int j = 0; j < PS; ++j) { pg[k][j] = 0.f; pb[k][j] = 0.f; }
+  float wv[NP][PS];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) vload<T, PS>(w + (k * 64 + lane) * PS, wv[k]);
+  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[NP][PS], xh[NP][PS];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int c = (k * 64 + lane) * PS;
+      float d[PS], xv[PS];
+      vload<T, PS>(dy + (int64_t)row * lddy + c, d);
+      vload<T, PS>(x + (int64_t)row * ldx + c, xv);
+#pragma unroll
+      for (int j = 0; j < PS; ++j) {
+        xh[k][j] = (xv[j] - mu) * rs;
+        g[k][j] = d[j] * wv[k][j];
+        s1 += g[k][j];
+        s2 += g[k][j] * xh[k][j];
+        pg[k][j] += d[j] * xh[k][j];
+        pb[k][j] += d[j];
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int c = (k * 64 + lane) * PS;
+      float o[PS];
+#pragma unroll
+      for (int j = 0; j < PS; ++j) o[j] = rs * (g[k][j] - s1 - xh[k][j] * s2);
+      if (dres) {
+        float r[PS];
+        vload<T, PS>(dres + (int64_t)row * ldres + c, r);
+#pragma unroll
+        for (int j = 0; j < PS; ++j) o[j] += r[j];
+      }
+      vstore<T, PS>(dx + (int64_t)row * lddx + c, o);
+    }
+  }
+  if (!ws) return;
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+#pragma unroll
+    for (int j = 0; j < PS; ++j) {
+      red[wave][0][(k * 64 + lane) * PS + j] = pg[k][j];
+      red[wave][1][(k * 64 + lane) * PS + j] = pb[k][j];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    ws[(int64_t)blockIdx.x * 2 * D + c] = a;
+    ws[(int64_t)blockIdx.x * 2 * D + D + c] = bb;
+  }
+}
+
+// out[c] (+)= sum_p ws[p*stride + c]   (deterministic second stage of every column sum)
+__global__ void reduce_partials_kernel(const float* ws, int64_t stride, int P, int D, float* out, int beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += ws[(int64_t)p * stride + c];
+  out[c] = beta ? out[c] + s : s;
+}
+
+// column partial sums of a [R, N] matrix: ws[chunk][N], chunk = blockIdx.y
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* x, int64_t ldx, int R, int N, int rows_per,
+                                                             float* ws) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    float v[4];
+    load4(x + (int64_t)r * ldx + c, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] += v[j];
+  }
+  store4(ws + (int64_t)blockIdx.y * N + c, s);
+}
+
+// periodic row sums: out[t][c] (+)= sum_b x[(b*period + t)*ldx + c]   (position-embedding grads)
+template <typename T>
+__global__ __launch_bounds__(256) void period_sum_kernel(const T* x, int64_t ldx, int nb, int period, int D,
+                                                         float* out, int beta) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int t = blockIdx.y;
+  if (c >= D) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < nb; ++b) {
+    float v[4];
+    load4(x + ((int64_t)b * period + t) * ldx + c, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] += v[j];
+  }
+  float* o = out + (int64_t)t * D + c;
+  if (beta) {
+    float ov[4];
+    load4(o, ov);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] += ov[j];
+  }
+  store4(o, s);
+}
+
+// x0[r] = tok[ids[r]] + pos[r % S]
+template <typename T>
+__global__ __launch_bounds__(256) void text_embed_kernel(const int64_t* ids, const T* tok, const T* pos, T* x0,
+                                                         int R, int S, int D, int V, int* bad) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  int64_t id = ids[row];
+  if (id < 0 || id >= V) { if (lane == 0) atomicOr(bad, 1); id = 0; }
+  const T* a = tok + id * D;
+  const T* p = pos + (int64_t)(row % S) * D;
+  for (int c = lane * 4; c < D; c += 256) {
+    float u[4], v[4];
+    load4(a + c, u);
+    load4(p + c, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) u[j] += v[j];
+    store4(x0 + (int64_t)row * D + c, u);
+  }
+}
+
+// ---- token-embedding backward: counting sort of ids, then one wave per distinct id.
+__global__ void id_count_kernel(const int64_t* ids, int R, int V, int* counts) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R && ids[r] >= 0 && ids[r] < V) atomicAdd(&counts[ids[r]], 1);
+}
+
+// exclusive scan of counts[V] -> offs[V+1], cursor[V] = offs[v]; one 1024-thread block.
+__global__ __launch_bounds__(1024) void id_scan_kernel(const int* counts, int V, int* offs, int* cursor) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (V + 1023) / 1024;
+  const int b = t * per, e = min(V, b + per);
+  int s = 0;
+  for (int v = b; v < e; ++v) s += counts[v];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    int add = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += add;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int v = b; v < e; ++v) {
+    offs[v] = run;
+    cursor[v] = run;
+    run += counts[v];
+  }
+  if (t == 1023) offs[V] = part[1023];
+}
+
+__global__ void id_place_kernel(const int64_t* ids, int R, int V, int* cursor, int* perm) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R && ids[r] >= 0 && ids[r] < V) perm[atomicAdd(&cursor[ids[r]], 1)] = r;
+}
+
+// gtok[v] (+)= sum of dx0 rows with id v; one wave per id
+template <typename T>
+__global__ __launch_bounds__(256) void id_segsum_kernel(const int* offs, const int* perm, const T* dx0, int D, int V,
+                                                        float* gtok, int beta) {
+  const int lane = threadIdx.x & 63;
+  const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const int b = offs[v], e = offs[v + 1];
+  if (b == e && beta) return;
+  for (int c = lane * 4; c < D; c += 256) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = b; i < e; ++i) {
+      float u[4];
+      load4(dx0 + (int64_t)perm[i] * D + c, u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += u[j];
+    }
+    float* o = gtok + (int64_t)v * D + c;
+    if (beta) {
+      float ov[4];
+      load4(o, ov);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += ov[j];
+    }
+    store4(o, s);
+  }
+}
+
+template <typename T, int PS, int NP>
+void ln_fwd_launch(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, const void* w, const void* b,
+                   float* mean, float* rstd, int R, int D, float eps, const void* pos, const void* cls, int period) {
+  hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP>), dim3((R + 3) / 4), dim3(256), 0, s, (T*)x, ldx, (T*)y, ldy,
+                     (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const T*)pos, (const T*)cls, period);
+}
+template <typename T, int PS, int NP>
+void ln_bwd_launch(hipStream_t s, int grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                   const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
+                   int64_t ldres, float* ws, int R, int D) {
+  hipLaunchKernelGGL((ln_bwd_kernel<T, PS, NP>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const T*)x, ldx,
+                     mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
+}
+
+// dispatch on (PS, NP) from D
+#define LN_DISPATCH(D, FN, T, ...)                                              \
+  do {                                                                          \
+    const int q_ = (D) / 64;                                                    \
+    if (q_ == 16) FN<T, 4, 4>(__VA_ARGS__);                                     \
+    else if (q_ == 12) FN<T, 4, 3>(__VA_ARGS__);                                \
+    else if (q_ == 8) FN<T, 4, 2>(__VA_ARGS__);                                 \
+    else if (q_ == 4) FN<T, 4, 1>(__VA_ARGS__);                                 \
+    else if (q_ == 2) FN<T, 2, 1>(__VA_ARGS__);                                 \
+    else if (q_ == 1) FN<T, 1, 1>(__VA_ARGS__);                                 \
+    else if (q_ == 6) FN<T, 2, 3>(__VA_ARGS__);                                 \
+    else if (q_ == 3) FN<T, 1, 3>(__VA_ARGS__);                                 \
+    else return clipmi_invalid("layernorm: unsupported hidden size");           \
+  } while (0)
+
+}  // namespace
+
+// ------------------------------------------------------------------------- C ABI
+extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy,
+                                    const void* w, const void* b, float* mean, float* rstd, int R, int D,
+                                    float eps, const void* pos, const void* cls, int period) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D % 64 == 0 && D <= 1024, "D must be a multiple of 64, <= 1024");
+  CLIPMI_REQUIRE(!pos || period > 0, "period");
+  if (R == 0) return CLIPMI_OK;
+  if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_fwd_launch, bf16, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+  else LN_DISPATCH(D, ln_fwd_launch, float, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// workspace: >= 2*D*nblk floats where nblk = min(1024, ceil(R/4)); clipmi_layernorm_bwd_ws
+extern "C" int64_t clipmi_layernorm_bwd_ws(int R, int D) {
+  int nb = (R + 3) / 4;
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  return (int64_t)nb * 2 * D * 4;
+}
+
+extern "C" int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx,
+                                    const void* dres, int64_t ldres, float* dw, float* db, int beta_wb,
+                                    void* ws, int64_t ws_bytes, int R, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D % 64 == 0 && D <= 1024, "D must be a multiple of 64, <= 1024");
+  if (R == 0) return CLIPMI_OK;
+  int nb = (R + 3) / 4;
+  if (nb > 1024) nb = 1024;
+  float* wsf = (dw || db) ? (float*)ws : nullptr;
+  if (wsf) CLIPMI_REQUIRE(ws_bytes >= (int64_t)nb * 2 * D * 4, "layernorm_bwd workspace too small");
+  if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  else LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  CLIPMI_CHECK_LAUNCH();
+  if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
+  if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int64_t clipmi_colsum_ws(int R, int N) {
+  int chunks = (R + 255) / 256;
+  if (chunks > 512) chunks = 512;
+  if (chunks < 1) chunks = 1;
+  return (int64_t)chunks * N * 4;
+}
+
+// out[n] (+)= sum_r x[r][n]   (bias gradients)
+extern "C" int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, int N, float* out, int beta,
+                             void* ws, int64_t ws_bytes) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(N % 4 == 0 && ldx % 4 == 0, "N, ldx must be multiples of 4");
+  int chunks = (R + 255) / 256;
+  if (chunks > 512) chunks = 512;
+  if (chunks < 1) chunks = 1;
+  CLIPMI_REQUIRE(ws_bytes >= (int64_t)chunks * N * 4, "colsum workspace too small");
+  int rows_per = (R + chunks - 1) / chunks;
+  dim3 g((N / 4 + 255) / 256, chunks);
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, R, N, rows_per, (float*)ws);
+  else hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, R, N, rows_per, (float*)ws);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 255) / 256), dim3(256), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_period_sum(void* stream, int dtype, const void* x, int64_t ldx, int nb, int period, int nt,
+                                 int D, float* out, int beta) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D % 4 == 0, "D % 4");
+  CLIPMI_REQUIRE(nt >= 1 && nt <= period, "nt must be in [1, period]");
+  dim3 g((D / 4 + 255) / 256, nt);
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(period_sum_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, nb, period, D, out, beta);
+  else hipLaunchKernelGGL(period_sum_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, nb, period, D, out, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_text_embed(void* stream, int dtype, const int64_t* ids, const void* tok, const void* pos,
+                                 void* x0, int R, int S, int D, int V, int* bad_flag) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D % 4 == 0, "D % 4");
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(text_embed_kernel<bf16>, dim3((R + 3) / 4), dim3(256), 0, s, ids, (const bf16*)tok, (const bf16*)pos, (bf16*)x0, R, S, D, V, bad_flag);
+  else hipLaunchKernelGGL(text_embed_kernel<float>, dim3((R + 3) / 4), dim3(256), 0, s, ids, (const float*)tok, (const float*)pos, (float*)x0, R, S, D, V, bad_flag);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// workspace (ints): counts[V] + offs[V+1] + cursor[V] + perm[R]
+extern "C" int64_t clipmi_text_embed_bwd_ws(int R, int V) { return ((int64_t)3 * V + 1 + R) * 4; }
+
+extern "C" int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids, const void* dx0, int R, int D, int V,
+                                     float* gtok, int beta, void* ws, int64_t ws_bytes) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(ws_bytes >= clipmi_text_embed_bwd_ws(R, V), "text_embed_bwd workspace too small");
+  CLIPMI_REQUIRE(D % 4 == 0, "D % 4");
+  int* counts = (int*)ws;
+  int* offs = counts + V;
+  int* cursor = offs + V + 1;
+  int* perm = cursor + V;
+  CLIPMI_HIP(hipMemsetAsync(counts, 0, (size_t)V * 4, s));
+  hipLaunchKernelGGL(id_count_kernel, dim3((R + 255) / 256), dim3(256), 0, s, ids, R, V, counts);
+  hipLaunchKernelGGL(id_scan_kernel, dim3(1), dim3(1024), 0, s, counts, V, offs, cursor);
+  hipLaunchKernelGGL(id_place_kernel, dim3((R + 255) / 256), dim3(256), 0, s, ids, R, V, cursor, perm);
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(id_segsum_kernel<bf16>, dim3((V + 3) / 4), dim3(256), 0, s, offs, perm, (const bf16*)dx0, D, V, gtok, beta);
+  else hipLaunchKernelGGL(id_segsum_kernel<float>, dim3((V + 3) / 4), dim3(256), 0, s, offs, perm, (const float*)dx0, D, V, gtok, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
