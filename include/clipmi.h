@@ -166,6 +166,15 @@ int clipmi_adamw(void* stream, float* p, const float* g, float* m, float* v, voi
                  double beta1, double beta2, double eps, double weight_decay, int step, const float* clip);
 int clipmi_cast_f32_bf16(void* stream, const float* src, void* dst, int64_t n);
 
+/* ---- Live kernel timing (bench.py roofline) --------------------------------------------------
+ * While armed, every launch whose variant label equals `variant` (e.g. "gemm_fwd_bias_qgelu_pre",
+ * "gemm_wgrad_splitk", "attn_fwd", "attn_bwd") is bracketed by hipEvents on its own stream,
+ * up to max_launches.  clipmi_prof_read (after a synchronize) returns the launch count and
+ * fills per-launch milliseconds and algorithmic FLOPs. */
+int clipmi_prof_arm(const char* variant, int max_launches);
+int clipmi_prof_disarm(void);
+int clipmi_prof_read(int max, float* ms, double* flops);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,7 +49,7 @@ class CLIPWithAdapters(nn.Module):
     def __init__(self, clip_model_name="openai/clip-vit-base-patch32", text_adapter_size=256,
                  vision_adapter_size=256, shared_adapter_layers=2, freeze_clip=True, use_text_adapter=True,
                  use_vision_adapter=True, use_shared_adapters=True, *, device=None, precision="bf16",
-                 pooling="first", init_seed=0, process_group=None):
+                 pooling="first", init_seed=0, process_group=None, fast_init=False):
         super().__init__()
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
@@ -69,7 +69,7 @@ class CLIPWithAdapters(nn.Module):
         self.clip.text_model.config = cfg.text_config
         self.clip.vision_model.config = cfg.vision_config
         self.processor = None  # tokenizer/image transform are host I/O, out of scope
-        self._load_clip_weights(clip_model_name, init_seed)
+        self._load_clip_weights(clip_model_name, init_seed, fast_init)
         text_hidden = cfg.text_config.hidden_size
         vision_hidden = cfg.vision_config.hidden_size
         self.use_text_adapter = use_text_adapter
@@ -95,8 +95,18 @@ class CLIPWithAdapters(nn.Module):
             self._freeze_clip_parameters()
 
     # ------------------------------------------------------------------ weights
-    def _load_clip_weights(self, name, seed):
+    def _load_clip_weights(self, name, seed, fast_init=False):
         path = os.path.join(str(name), "model.safetensors")
+        if fast_init and not os.path.isfile(path):
+            # benchmark init: same per-tensor HF init scales, drawn on the device by torch's
+            # generator (not bit-identical to clipmi.synth, which the parity tests use)
+            g = torch.Generator(device=self.clip.arena.device).manual_seed(seed)
+            with torch.no_grad():
+                for pname, shape, std, mean in synth.clip_param_specs(self.config):
+                    p = self.clip.arena.params[pname]
+                    p.normal_(mean, std, generator=g)
+                self.clip.logit_scale.fill_(C.LN100)
+            return
         if os.path.isfile(path):
             from safetensors.torch import load_file
             sd = load_file(path, device="cpu")

@@ -522,7 +522,9 @@ class ContrastiveFn(torch.autograd.Function):
             dist.all_reduce(loss_out, group=group)
         else:
             loss_out = loss
-        ctx.save = (th, ih, tn, inn, tg, ig, lt, li, lse, ls)
+        # outputs (th, ih, lt, li) must go through save_for_backward: keeping them as plain ctx
+        # attributes forms node -> ctx -> output -> grad_fn -> node, a cycle that leaks the graph
+        ctx.save_for_backward(th, ih, tn, inn, tg, ig, lt, li, lse, ls)
         ctx.group, ctx.world, ctx.B, ctx.Bg, ctx.lab0 = group, world, B, Bg, lab0
         ctx.ls_param, ctx.arena = logit_scale, arena
         ctx.mark_non_differentiable(lt, li)
@@ -530,7 +532,7 @@ class ContrastiveFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss, gth, gih, glt, gli):
-        th, ih, tn, inn, tg, ig, lt, li, lse, ls = ctx.save
+        th, ih, tn, inn, tg, ig, lt, li, lse, ls = ctx.saved_tensors
         B, Bg, E, world = ctx.B, ctx.Bg, th.shape[1], ctx.world
         dev = th.device
         s = K.stream()

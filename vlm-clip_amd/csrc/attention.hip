@@ -482,9 +482,14 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
   CLIPMI_REQUIRE(N >= 1 && N <= 256, "N must be in [1, 256]");
   if (B == 0) return CLIPMI_OK;
+  const int npad = (N + 31) & ~31;
+  // algorithmic FLOPs: QK^T and PV over the padded key range, B*H heads
+  const double flops = 4.0 * B * H * (double)N * npad * 64;
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
+    ProfScope ps(s, "attn_fwd", flops);
     CLIPMI_TRY(causal ? fwd_dispatch<true>(p, s) : fwd_dispatch<false>(p, s));
+    ps.finish("attn_fwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, causal, 0.125f};
     size_t lds = (size_t)N * 64 * 4 * 2 + N * 4;
@@ -516,8 +521,11 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
       CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr = true;
     }
+    const double flops = 10.0 * B * H * (double)N * npad * 64;
+    ProfScope ps(s, nullptr, flops);
     if (causal) hipLaunchKernelGGL(attn_bwd_mfma<true>, dim3(B * H), dim3(512), lds, s, p);
     else hipLaunchKernelGGL(attn_bwd_mfma<false>, dim3(B * H), dim3(512), lds, s, p);
+    ps.finish("attn_bwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D, causal, 0.125f};
     size_t lds = (size_t)N * 64 * 4 * 2 + N * 12;

@@ -64,9 +64,9 @@ __device__ __forceinline__ void st4(OutT* p, const float v[4], int nv, bool vec)
     if (j < nv) p[j] = from_f32<OutT>(v[j]);
 }
 
-template <typename OutT>
+template <typename OutT, int EPI>
 __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[4]) {
-  const int f = p.flags;
+  const int f = EPI >= 0 ? EPI : p.flags;  // EPI >= 0: flags folded at compile time
   const int nv = min(4, p.N - n);
   const bool vec = p.vec && nv == 4;
 #pragma unroll
@@ -177,7 +177,7 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int kk, int
   }
 }
 
-template <bool AK, bool BKM, typename OutT>
+template <bool AK, bool BKM, typename OutT, int EPI>
 __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
       if (p.ws) {
         st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
       } else {
-        epilogue4<OutT>(p, m, n, v);
+        epilogue4<OutT, EPI>(p, m, n, v);
       }
     }
   }
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p, int akm, int bkm
     if (m >= p.M || n >= p.N) continue;
     float v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
     if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
-    else epilogue4<OutT>(p, m, n, v);
+    else epilogue4<OutT, -1>(p, m, n, v);
   }
 }
 
@@ -331,9 +331,60 @@ __global__ void splitk_reduce_kernel(const float* ws, float* C, int64_t ldc, int
   }
 }
 
-template <bool AK, bool BKM, typename OutT>
+template <bool AK, bool BKM, typename OutT, int EPI>
 void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT, EPI>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
+}
+
+constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU, E_G = CLIPMI_EPI_GELU;
+constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU, E_DG = CLIPMI_EPI_DGELU, E_BETA = CLIPMI_EPI_BETA;
+
+// Specialised epilogues for the combinations the CLIP path issues; anything else takes the
+// runtime-flag instance.  Returns the variant label (also used by the live profiler).
+const char* dispatch_bf16(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags) {
+  if (p.ws) {
+    if (sel == 0) { launch_bf16<false, false, float, 0>(p, splits, s); return "gemm_wgrad_splitk"; }
+    launch_bf16<true, true, float, -1>(p, splits, s);
+    return "gemm_generic";
+  }
+  if (sel == 3 && !f32o) {
+    switch (flags) {
+      case E_B: launch_bf16<true, true, bf16, E_B>(p, splits, s); return "gemm_fwd_bias";
+      case E_B | E_R: launch_bf16<true, true, bf16, E_B | E_R>(p, splits, s); return "gemm_fwd_bias_resid";
+      case E_B | E_Q | E_P: launch_bf16<true, true, bf16, E_B | E_Q | E_P>(p, splits, s); return "gemm_fwd_bias_qgelu_pre";
+      case E_B | E_Q: launch_bf16<true, true, bf16, E_B | E_Q>(p, splits, s); return "gemm_fwd_bias_qgelu";
+      case E_B | E_G | E_P: launch_bf16<true, true, bf16, E_B | E_G | E_P>(p, splits, s); return "gemm_fwd_bias_gelu_pre";
+      case E_B | E_G: launch_bf16<true, true, bf16, E_B | E_G>(p, splits, s); return "gemm_fwd_bias_gelu";
+      case 0: launch_bf16<true, true, bf16, 0>(p, splits, s); return "gemm_fwd";
+      default: break;
+    }
+  }
+  if (sel == 2 && !f32o) {
+    switch (flags) {
+      case 0: launch_bf16<true, false, bf16, 0>(p, splits, s); return "gemm_dgrad";
+      case E_DQ: launch_bf16<true, false, bf16, E_DQ>(p, splits, s); return "gemm_dgrad_dqgelu";
+      case E_DG: launch_bf16<true, false, bf16, E_DG>(p, splits, s); return "gemm_dgrad_dgelu";
+      case E_R: launch_bf16<true, false, bf16, E_R>(p, splits, s); return "gemm_dgrad_resid";
+      default: break;
+    }
+  }
+  if (sel == 0 && f32o && flags == E_BETA) { launch_bf16<false, false, float, E_BETA>(p, splits, s); return "gemm_wgrad"; }
+  if (f32o) {
+    switch (sel) {
+      case 3: launch_bf16<true, true, float, -1>(p, splits, s); break;
+      case 2: launch_bf16<true, false, float, -1>(p, splits, s); break;
+      case 1: launch_bf16<false, true, float, -1>(p, splits, s); break;
+      default: launch_bf16<false, false, float, -1>(p, splits, s); break;
+    }
+  } else {
+    switch (sel) {
+      case 3: launch_bf16<true, true, bf16, -1>(p, splits, s); break;
+      case 2: launch_bf16<true, false, bf16, -1>(p, splits, s); break;
+      case 1: launch_bf16<false, true, bf16, -1>(p, splits, s); break;
+      default: launch_bf16<false, false, bf16, -1>(p, splits, s); break;
+    }
+  }
+  return "gemm_generic";
 }
 
 }  // namespace
@@ -381,29 +432,21 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }
   p.tiles_n = (d->N + tile - 1) / tile;
   p.ntiles = p.tiles_n * ((d->M + tile - 1) / tile);
+  const double flops = 2.0 * d->M * d->N * d->K;
   if (bf) {
     const bool f32o = d->c_dtype == CLIPMI_F32 || p.ws;
     const int sel = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
-    if (f32o) {
-      switch (sel) {
-        case 3: launch_bf16<true, true, float>(p, splits, s); break;
-        case 2: launch_bf16<true, false, float>(p, splits, s); break;
-        case 1: launch_bf16<false, true, float>(p, splits, s); break;
-        default: launch_bf16<false, false, float>(p, splits, s); break;
-      }
-    } else {
-      switch (sel) {
-        case 3: launch_bf16<true, true, bf16>(p, splits, s); break;
-        case 2: launch_bf16<true, false, bf16>(p, splits, s); break;
-        case 1: launch_bf16<false, true, bf16>(p, splits, s); break;
-        default: launch_bf16<false, false, bf16>(p, splits, s); break;
-      }
-    }
+    // the label is only known after dispatch; probe the profiler with the would-be label first
+    ProfScope ps(s, nullptr, 0.0);
+    const char* label = dispatch_bf16(p, splits, s, f32o, sel, d->flags);
+    ps.finish(label, flops);
   } else {
+    ProfScope ps(s, nullptr, 0.0);
     if (d->c_dtype == CLIPMI_F32 || p.ws)
       hipLaunchKernelGGL(gemm_f32_kernel<float>, dim3(p.ntiles, splits), dim3(256), 0, s, p, d->a_kmajor, d->b_kmajor);
     else
       hipLaunchKernelGGL(gemm_f32_kernel<bf16>, dim3(p.ntiles, splits), dim3(256), 0, s, p, d->a_kmajor, d->b_kmajor);
+    ps.finish("gemm_f32", flops);
   }
   CLIPMI_CHECK_LAUNCH();
   if (p.ws) {

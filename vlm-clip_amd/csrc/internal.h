@@ -12,3 +12,13 @@ void clipmi_set_error(const std::string& msg);
 #define CLIPMI_REQUIRE(cond, msg) do { if (!(cond)) return clipmi_invalid(std::string(__func__) + ": " + (msg)); } while (0)
 #define CLIPMI_HIP(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return clipmi_fail(e_, __FILE__, __LINE__); } while (0)
 #define CLIPMI_TRY(call) do { int s_ = (call); if (s_ != CLIPMI_OK) return s_; } while (0)
+
+// ---- live kernel profiler (clipmi_prof_*): while armed for a variant label, launches with
+// that label are bracketed by hipEvents on their own stream, so a caller can time one kernel
+// family inside a real step without host synchronisation.
+struct ProfScope {
+  hipStream_t s;
+  int slot;
+  ProfScope(hipStream_t stream, const char* label, double flops);
+  void finish(const char* label, double flops);
+};
