@@ -36,8 +36,12 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("akm,bkm", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 136, 72), (77, 64, 768), (1000, 512, 200)])
-def test_gemm_layouts(dtype, akm, bkm, M, N, K):
+@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 136, 72), (77, 64, 768), (1000, 512, 200),
+                                   (1000, 776, 768), (600, 264, 1000), (512, 256, 64)])
+def test_gemm_layouts(dtype, akm, bkm, M, N, K, small):
+    if dtype == torch.float32 and small:
+        pytest.skip("tile choice only applies to the bf16 path")
     if dtype == torch.bfloat16 and (not akm) and M % 8:
         pytest.skip("row-major A needs M % 8 == 0")
     if dtype == torch.bfloat16 and (akm or bkm) and K % 8:
@@ -45,7 +49,9 @@ def test_gemm_layouts(dtype, akm, bkm, M, N, K):
     A = _mk((M, K) if akm else (K, M), dtype, 1)
     B = _mk((N, K) if bkm else (K, N), dtype, 2)
     C = torch.empty(M, N, device="cuda", dtype=torch.float32)
-    kern.gemm(M, N, K, A, A.stride(0), akm, B, B.stride(0), bkm, C, N)
+    if dtype == torch.bfloat16 and (not bkm) and N % 8:
+        pytest.skip("row-major B needs N % 8 == 0")
+    kern.gemm(M, N, K, A, A.stride(0), akm, B, B.stride(0), bkm, C, N, small_tile=small)
     Af = (A if akm else A.t()).float()
     Bf = (B if bkm else B.t()).float()
     ref = Af @ Bf.t()
@@ -93,3 +99,22 @@ def test_gemm_splitk_wgrad(dtype):
     ref = c0 + dY.float().t() @ X.float()
     torch.cuda.synchronize()
     assert (C - ref).abs().max().item() / ref.abs().max().item() < (1e-4 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("T,Nout,Kin,split", [(3000, 256, 192, 8), (50000, 768, 3072, 12), (77, 64, 128, 1),
+                                              (20000, 2304, 768, 4)])
+def test_wgrad_fused_bias_grad(T, Nout, Kin, split):
+    """256 wgrad kernel with the fused bias gradient (sum over tokens of dY)."""
+    dY = _mk((T, Nout), torch.bfloat16, 12)
+    X = _mk((T, Kin), torch.bfloat16, 13)
+    C = _mk((Nout, Kin), torch.float32, 14)
+    db = _mk((Nout,), torch.float32, 15)
+    c0, db0 = C.clone(), db.clone()
+    ws = torch.empty(max(1, split) * Nout * Kin, device="cuda", dtype=torch.float32)
+    kern.gemm(Nout, Kin, T, dY, Nout, False, X, Kin, False, C, Kin, flags=_lib.EPI_BETA, split_k=split,
+              workspace=ws, bias_grad=db)
+    ref = c0 + dY.float().t() @ X.float()
+    dref = db0 + dY.float().sum(0)
+    torch.cuda.synchronize()
+    assert (C - ref).abs().max().item() / ref.abs().max().item() < 1e-2
+    assert (db - dref).abs().max().item() / dref.abs().max().item() < 1e-3

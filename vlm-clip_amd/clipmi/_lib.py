@@ -30,7 +30,8 @@ class GemmDesc(ctypes.Structure):
                 ("flags", ctypes.c_int),
                 ("ab_dtype", ctypes.c_int), ("c_dtype", ctypes.c_int), ("bias_dtype", ctypes.c_int),
                 ("split_k", ctypes.c_int),
-                ("workspace", c_vp), ("workspace_bytes", c_i64)]
+                ("workspace", c_vp), ("workspace_bytes", c_i64),
+                ("bias_grad", c_vp), ("force_small_tile", ctypes.c_int)]
 
 
 class ClipmiError(RuntimeError):

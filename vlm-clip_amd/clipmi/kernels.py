@@ -37,7 +37,7 @@ def _on_gpu(*ts):
 
 
 def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, residual=None, ldr=0,
-         aux=None, ldaux=0, alpha=1.0, flags=0, split_k=1, workspace=None):
+         aux=None, ldaux=0, alpha=1.0, flags=0, split_k=1, workspace=None, bias_grad=None, small_tile=False):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see include/clipmi.h clipmi_gemm."""
     _on_gpu(A, B, C, bias, residual, aux, workspace)
     if A.dtype != B.dtype:
@@ -54,6 +54,8 @@ def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, resi
     d.ab_dtype, d.c_dtype = dt(A), dt(C)
     d.bias_dtype = dt(bias) if bias is not None else F32
     d.split_k = split_k
+    d.bias_grad = bias_grad.data_ptr() if bias_grad is not None else None
+    d.force_small_tile = int(small_tile)
     if workspace is not None:
         d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     _lib.check(_lib.lib().clipmi_gemm(stream(), ctypes.byref(d)), "clipmi_gemm")

@@ -401,15 +401,20 @@ class AdapterFn(torch.autograd.Function):
         else:
             dz = dy2
         cws = _ws(_lib.lib().clipmi_colsum_ws(R, max(Dh, A)), dev)
+        bf = dtype == torch.bfloat16
         if train_params:
-            K.gemm(Dh, A, R, dz, Dh, False, act, A, False, arena.view(f"{up}.weight", g), A, flags=_lib.EPI_BETA)
-            call("clipmi_colsum", s, dc, P_(dz), Dh, R, Dh, arena.ptr(f"{up}.bias", g), 1, P_(cws), cws.numel())
+            K.gemm(Dh, A, R, dz, Dh, False, act, A, False, arena.view(f"{up}.weight", g), A, flags=_lib.EPI_BETA,
+                   bias_grad=arena.view(f"{up}.bias", g) if bf else None)
+            if not bf:
+                call("clipmi_colsum", s, dc, P_(dz), Dh, R, Dh, arena.ptr(f"{up}.bias", g), 1, P_(cws), cws.numel())
         dpre = torch.empty(R, A, dtype=dtype, device=dev)
         K.gemm(R, A, Dh, dz, Dh, True, arena.view(f"{up}.weight", wbuf), A, False, dpre, A, aux=pre, ldaux=A,
                flags=_lib.EPI_DGELU)
         if train_params:
-            K.gemm(A, Dh, R, dpre, A, False, x2, Dh, False, arena.view(f"{dn}.weight", g), Dh, flags=_lib.EPI_BETA)
-            call("clipmi_colsum", s, dc, P_(dpre), A, R, A, arena.ptr(f"{dn}.bias", g), 1, P_(cws), cws.numel())
+            K.gemm(A, Dh, R, dpre, A, False, x2, Dh, False, arena.view(f"{dn}.weight", g), Dh, flags=_lib.EPI_BETA,
+                   bias_grad=arena.view(f"{dn}.bias", g) if bf else None)
+            if not bf:
+                call("clipmi_colsum", s, dc, P_(dpre), A, R, A, arena.ptr(f"{dn}.bias", g), 1, P_(cws), cws.numel())
         dx = torch.empty(R, Dh, dtype=dtype, device=dev)
         K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
                flags=_lib.EPI_RESID)

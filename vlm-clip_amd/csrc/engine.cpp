@@ -40,7 +40,7 @@ int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb,
          bool bkm, void* C, int64_t ldc, int c_dt, int flags, const void* bias = nullptr, const void* res = nullptr,
          int64_t ldr = 0, void* aux = nullptr, int64_t ldaux = 0, int split = 1, void* ws = nullptr,
-         int64_t ws_bytes = 0) {
+         int64_t ws_bytes = 0, float* bias_grad = nullptr) {
   clipmi_gemm_desc d;
   memset(&d, 0, sizeof(d));
   d.M = M; d.N = N; d.K = K;
@@ -51,14 +51,16 @@ int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool 
   d.alpha = 1.f; d.flags = flags;
   d.ab_dtype = dt; d.c_dtype = c_dt; d.bias_dtype = dt;
   d.split_k = split; d.workspace = ws; d.workspace_bytes = ws_bytes;
+  d.bias_grad = bias_grad;
   return clipmi_gemm(s, &d);
 }
 
 // split-K factor for a wgrad GEMM [M x N] reducing over K tokens
 int wgrad_splits(int M, int N, int K, int dt) {
-  const int tile = dt == CLIPMI_BF16 ? 128 : 64;
+  const int tile = dt == CLIPMI_BF16 ? 256 : 64;
+  const int target = dt == CLIPMI_BF16 ? 512 : 1024;  // workgroups: 2 waves of the 256-CU chip
   const int tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
-  int s = std::max(1, 1024 / std::max(1, tiles));
+  int s = std::max(1, target / std::max(1, tiles));
   s = std::min(s, 32);
   while (s > 1 && (int64_t)K / s < 512) --s;
   return s;
@@ -147,10 +149,16 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
   const int64_t col_bytes = p.ln - p.colsum;
   const int64_t ln_bytes = p.total - p.ln;
   const int f32 = CLIPMI_F32;
-  auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C) {
+  // wgrad: C[M,N] += sum_tokens A[t][m] B[t][n]; the bf16 path also fuses the Linear bias
+  // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
+  auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
+                   float* bgrad) -> int {
     const int sp = wgrad_splits(M, N, R, dt);
-    return gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
-                nullptr, 0, sp, wsplit, split_bytes);
+    const bool fuse = dt == CLIPMI_BF16;
+    CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
+                    nullptr, 0, sp, wsplit, split_bytes, fuse ? bgrad : nullptr));
+    if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
+    return CLIPMI_OK;
   };
   for (int l = d->L - 1; l >= 0; --l) {
     const clipmi_layer_w& w = d->layers[l];
@@ -160,21 +168,17 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
     // MLP branch: dx is dL/dy
     CLIPMI_TRY(gemm(s, dt, R, F, D, dx, D, true, w.fc2_w, F, false, dbig, F, dt, CLIPMI_EPI_DQGELU, nullptr, nullptr,
                     0, a.pre, F));                                          // d_pre = (dx W2) * qgelu'(pre)
-    CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w));                     // gW2 += dx^T act
-    CLIPMI_TRY(clipmi_colsum(s, dt, dx, D, R, D, g.fc2_b, 1, wcol, col_bytes));
-    CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w));                   // gW1 += d_pre^T ln2
-    CLIPMI_TRY(clipmi_colsum(s, dt, dbig, F, R, F, g.fc1_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w, g.fc2_b));            // gW2 += dx^T act, gb2 += sum dx
+    CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w, g.fc1_b));          // gW1 += d_pre^T ln2
     CLIPMI_TRY(gemm(s, dt, R, D, F, dbig, F, true, w.fc1_w, D, false, dln, D, dt, 0));  // d_ln2 = d_pre W1
     CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx, D, g.ln2_w, g.ln2_b,
                                     1, wln, ln_bytes, R, D));              // dh = dx + LN2'(d_ln2)
     // attention branch: g2 is dL/dh
     CLIPMI_TRY(gemm(s, dt, R, D, D, g2, D, true, w.out_w, D, false, dln, D, dt, 0));     // d_o = dh Wo
-    CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w));                                     // gWo += dh^T o
-    CLIPMI_TRY(clipmi_colsum(s, dt, g2, D, R, D, g.out_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w, g.out_b));                            // gWo += dh^T o
     CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
                                     d->N, D));                              // d_qkv
-    CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w));           // gWqkv += d_qkv^T ln1
-    CLIPMI_TRY(clipmi_colsum(s, dt, dbig, 3 * D, R, 3 * D, g.qkv_b, 1, wcol, col_bytes));
+    CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w, g.qkv_b));  // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
     CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
                                     g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)

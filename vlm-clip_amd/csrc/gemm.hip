@@ -262,6 +262,153 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
   }
 }
 
+// ------------------------------------------------------------------ 256x256 LDS-DMA path
+// 512 threads = 8 waves (2 along M x 4 along N), each wave 128x64 = 8x4 MFMA tiles
+// (128 accumulator VGPRs).  Tiles arrive by LDS-DMA (buffer_load ... lds, 16 B per lane,
+// 1 KiB per wave-instruction): the LDS images are lane-linear, so the XOR swizzle is
+// applied to the per-lane SOURCE address and undone by the same read-side swizzle as the
+// 128 kernel.  Two 64 KiB buffers: the DMA of k-step t+1 is in flight while k-step t's
+// 64 MFMAs per wave run; one vmcnt(0) + barrier per k-step.  Buffer descriptors are
+// rebuilt per k-step at the slab start with exact byte extents, so rows past M/N/K read
+// as zero (no clamping, no branches) and offsets stay 32-bit for any tensor size.
+// BIASGRAD (wgrad only): waves with wn == 0 of n-tile 0 add one MFMA per A fragment
+// against a ones fragment, producing sum_k A(m,k) = the Linear bias gradient.
+constexpr int BT = 256, NT2 = 512;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+// stage one 256x64 operand tile of k-step at k0 into an LDS image (32 KiB)
+template <bool KMAJ>
+__device__ __forceinline__ void stage256(char* img, const bf16* X, int64_t ld, int row0, int R, int k0, int K,
+                                         int wave, int lane) {
+  if (KMAJ) {
+    // rows row0.. (<=256 valid), k0..k0+63; each wave-instruction fills 8 rows x 128 B
+    const int rows = min(BT, R - row0);
+    const bf16* base = X + (int64_t)row0 * ld + k0;
+    const uint32_t rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;
+      const int r = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      dma16(rs, img + j * 1024, (int)((int64_t)r * ld * 2 + c * 16));
+    }
+  } else {
+    // k rows k0..k0+63 (<= K), columns row0..row0+255 as two 128-wide half images [64][128]
+    const int krows = min(64, K - k0);
+    const int cols = min(BT, R - row0);
+    const bf16* base = X + (int64_t)k0 * ld + row0;
+    const uint32_t rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;            // 0..31
+      const int half = j >> 4;
+      const int kr = 4 * (j & 15) + (lane >> 4);
+      const int c = (lane & 15) ^ mimg_swz(kr);
+      dma16(rs, img + half * 16384 + (j & 15) * 1024, (int)((int64_t)kr * ld * 2 + (half * 128 + c * 8) * 2));
+    }
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 read_frag256(const char* img, int rb, int kk, int lane) {
+  if (KMAJ) return read_frag<true>(img, rb, kk, lane);
+  return read_frag<false>(img + (rb >> 7) * 16384, rb & 127, kk, lane);
+}
+
+template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD>
+__global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_grad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tile = xcd_remap(blockIdx.x, p.ntiles);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const bf16* A = (const bf16*)p.A;
+  const bf16* B = (const bf16*)p.B;
+  const int Kv = kend;  // rows/cols past the split end read as zero
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[8];
+  const bool do_bias = BIASGRAD && tn == 0 && wn == 0;
+  if (BIASGRAD) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+
+#define IMG_A(b) (smem + (b) * 65536)
+#define IMG_B(b) (smem + (b) * 65536 + 32768)
+  if (nk > 0) {
+    stage256<AK>(IMG_A(0), A, p.lda, m0, p.M, kbeg, Kv, wave, lane);
+    stage256<BKM>(IMG_B(0), B, p.ldb, n0, p.N, kbeg, Kv, wave, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) {
+      const int k1 = kbeg + (it + 1) * BK;
+      stage256<AK>(IMG_A(cur ^ 1), A, p.lda, m0, p.M, k1, Kv, wave, lane);
+      stage256<BKM>(IMG_B(cur ^ 1), B, p.ldb, n0, p.N, k1, Kv, wave, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[8], fb[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = read_frag256<AK>(IMG_A(cur), wm * 128 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag256<BKM>(IMG_B(cur), wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      if (BIASGRAD && do_bias) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fa[i], accb[i], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef IMG_A
+#undef IMG_B
+
+  if (BIASGRAD && do_bias && lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + lane;
+      if (m < p.M) atomicAdd(bias_grad + m, accb[i][0]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
+      else epilogue4<OutT, EPI>(p, m, n, v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ f32 SIMT path
 constexpr int FT = 64, FK = 16;
 
@@ -336,8 +483,52 @@ void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT, EPI>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
 }
 
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
+  static bool attr = false;  // 128 KiB of dynamic LDS needs the opt-in once per instance
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, OutT, EPI, BG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG>), dim3(p.ntiles, splits), dim3(NT2), 131072, s, p,
+                     bias_grad);
+}
+
 constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU, E_G = CLIPMI_EPI_GELU;
 constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU, E_DG = CLIPMI_EPI_DGELU, E_BETA = CLIPMI_EPI_BETA;
+
+const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
+  if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
+    if (p.ws) {
+      if (bg) launch256<false, false, float, 0, true>(p, splits, s, bg);
+      else launch256<false, false, float, 0, false>(p, splits, s, bg);
+      return "gemm256_wgrad_splitk";
+    }
+    if (bg) launch256<false, false, float, E_BETA, true>(p, splits, s, bg);
+    else launch256<false, false, float, E_BETA, false>(p, splits, s, bg);
+    return "gemm256_wgrad";
+  }
+  if (bg) return nullptr;
+  if (sel == 3 && !f32o) {
+    switch (flags) {
+      case E_B: launch256<true, true, bf16, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias";
+      case E_B | E_R: launch256<true, true, bf16, E_B | E_R, false>(p, splits, s, bg); return "gemm256_fwd_bias_resid";
+      case E_B | E_Q | E_P: launch256<true, true, bf16, E_B | E_Q | E_P, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu_pre";
+      case E_B | E_Q: launch256<true, true, bf16, E_B | E_Q, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu";
+      case 0: launch256<true, true, bf16, 0, false>(p, splits, s, bg); return "gemm256_fwd";
+      default: break;
+    }
+  }
+  if (sel == 2 && !f32o) {
+    switch (flags) {
+      case 0: launch256<true, false, bf16, 0, false>(p, splits, s, bg); return "gemm256_dgrad";
+      case E_DQ: launch256<true, false, bf16, E_DQ, false>(p, splits, s, bg); return "gemm256_dgrad_dqgelu";
+      default: break;
+    }
+  }
+  return nullptr;  // not specialised: use the 128 kernel
+}
 
 // Specialised epilogues for the combinations the CLIP path issues; anything else takes the
 // runtime-flag instance.  Returns the variant label (also used by the live profiler).
@@ -416,7 +607,12 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.ws = nullptr;
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
           ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
-  const int tile = bf ? BM : FT;
+  // 256x256 LDS-DMA kernel for the big shapes (k-major operands need K % 64 == 0: the
+  // buffer range check zero-fills rows, not a row's k tail)
+  const bool kok = (!d->a_kmajor || d->K % 64 == 0) && (!d->b_kmajor || d->K % 64 == 0);
+  const bool use256 = bf && kok && ((d->M >= 256 && d->N >= 128) || d->bias_grad) && !d->force_small_tile;
+  CLIPMI_REQUIRE(!d->bias_grad || use256, "bias_grad fusion needs the 256 kernel (bf16, wgrad layout)");
+  const int tile = bf ? (use256 ? BT : BM) : FT;
   const int kstep = bf ? BK : FK;
   if (splits > 1) {
     CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32, "split_k needs fp32 C");
@@ -438,7 +634,20 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     const int sel = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
     // the label is only known after dispatch; probe the profiler with the would-be label first
     ProfScope ps(s, nullptr, 0.0);
-    const char* label = dispatch_bf16(p, splits, s, f32o, sel, d->flags);
+    const char* label = nullptr;
+    if (use256) {
+      GemmP q = p;
+      q.tiles_n = (d->N + BT - 1) / BT;
+      q.ntiles = q.tiles_n * ((d->M + BT - 1) / BT);
+      label = dispatch256(q, splits, s, f32o, sel, d->flags, d->bias_grad);
+    }
+    if (!label) {
+      CLIPMI_REQUIRE(!d->bias_grad, "bias_grad needs the wgrad layout (both operands row-major in k)");
+      GemmP q = p;  // 128-tile grid (p's tile counts may be sized for the 256 kernel)
+      q.tiles_n = (d->N + BM - 1) / BM;
+      q.ntiles = q.tiles_n * ((d->M + BM - 1) / BM);
+      label = dispatch_bf16(q, splits, s, f32o, sel, d->flags);
+    }
     ps.finish(label, flops);
   } else {
     ProfScope ps(s, nullptr, 0.0);

@@ -170,12 +170,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
 }
 
 // out[c] (+)= sum_p ws[p*stride + c]   (deterministic second stage of every column sum)
-__global__ void reduce_partials_kernel(const float* ws, int64_t stride, int P, int D, float* out, int beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += ws[(int64_t)p * stride + c];
-  out[c] = beta ? out[c] + s : s;
+// block = 64 columns x 16 partial groups; fixed summation order -> bitwise reproducible
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* ws, int64_t stride, int P, int D,
+                                                               float* out, int beta) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < D) {
+    int p = ty;
+    for (; p + 16 < P; p += 32) {
+      s0 += ws[(int64_t)p * stride + c];
+      s1 += ws[(int64_t)(p + 16) * stride + c];
+    }
+    if (p < P) s0 += ws[(int64_t)p * stride + c];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && c < D) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    out[c] = beta ? out[c] + s : s;
+  }
 }
 
 // column partial sums of a [R, N] matrix: ws[chunk][N], chunk = blockIdx.y
@@ -240,10 +257,32 @@ __global__ __launch_bounds__(256) void text_embed_kernel(const int64_t* ids, con
   }
 }
 
-// ---- token-embedding backward: counting sort of ids, then one wave per distinct id.
+// ---- token-embedding backward: counting sort of ids (wave-aggregated atomics: runs of equal
+// ids, e.g. EOS padding, take one atomic per run), then fixed 64-row chunks of the sorted
+// order are summed by one wave each, flushing a partial row sum whenever the id changes.
+// Work per wave is bounded however skewed the id histogram is (a padding id can own half
+// the batch).
+struct Run {
+  int id, leader, len;
+};
+__device__ __forceinline__ Run lane_run(int id, int lane) {
+  int prev = __shfl_up(id, 1, 64);
+  const bool start = lane == 0 || id != prev;
+  const unsigned long long starts = __ballot(start);
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  const int leader = 63 - __builtin_clzll(starts & upto);
+  const unsigned long long after = starts & ~upto;
+  const int next = after ? __builtin_ctzll(after) : 64;
+  return Run{id, leader, next - lane};
+}
+
 __global__ void id_count_kernel(const int64_t* ids, int R, int V, int* counts) {
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < R && ids[r] >= 0 && ids[r] < V) atomicAdd(&counts[ids[r]], 1);
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int id = -1;
+  if (r < R && ids[r] >= 0 && ids[r] < V) id = (int)ids[r];
+  const Run run = lane_run(id, lane);
+  if (run.leader == lane && id >= 0) atomicAdd(&counts[id], run.len);
 }
 
 // exclusive scan of counts[V] -> offs[V+1], cursor[V] = offs[v]; one 1024-thread block.
@@ -271,36 +310,47 @@ __global__ __launch_bounds__(1024) void id_scan_kernel(const int* counts, int V,
   if (t == 1023) offs[V] = part[1023];
 }
 
-__global__ void id_place_kernel(const int64_t* ids, int R, int V, int* cursor, int* perm) {
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < R && ids[r] >= 0 && ids[r] < V) perm[atomicAdd(&cursor[ids[r]], 1)] = r;
+__global__ void id_place_kernel(const int64_t* ids, int R, int V, int* cursor, int* perm, int* sorted_id) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int id = -1;
+  if (r < R && ids[r] >= 0 && ids[r] < V) id = (int)ids[r];
+  const Run run = lane_run(id, lane);
+  int base = 0;
+  if (run.leader == lane && id >= 0) base = atomicAdd(&cursor[id], run.len);
+  base = __shfl(base, run.leader, 64);
+  if (id >= 0) {
+    perm[base + lane - run.leader] = r;
+    sorted_id[base + lane - run.leader] = id;
+  }
 }
 
-// gtok[v] (+)= sum of dx0 rows with id v; one wave per id
+// one wave per 64 sorted rows; gtok[id] += rows of that id (fp32 atomics at id changes)
 template <typename T>
-__global__ __launch_bounds__(256) void id_segsum_kernel(const int* offs, const int* perm, const T* dx0, int D, int V,
-                                                        float* gtok, int beta) {
+__global__ __launch_bounds__(256) void id_chunk_sum_kernel(const int* perm, const int* sorted_id, const int* nvalid,
+                                                           const T* dx0, int D, float* gtok) {
+  const int n = *nvalid;  // rows with an in-vocabulary id (offs[V])
   const int lane = threadIdx.x & 63;
-  const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (v >= V) return;
-  const int b = offs[v], e = offs[v + 1];
-  if (b == e && beta) return;
-  for (int c = lane * 4; c < D; c += 256) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = c * 64, e = min(n, b + 64);
+  if (b >= n) return;
+  for (int c0 = lane * 4; c0 < D; c0 += 256) {
     float s[4] = {0.f, 0.f, 0.f, 0.f};
+    int cur = sorted_id[b];
     for (int i = b; i < e; ++i) {
+      const int id = sorted_id[i];
+      if (id != cur) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { atomicAdd(gtok + (int64_t)cur * D + c0 + j, s[j]); s[j] = 0.f; }
+        cur = id;
+      }
       float u[4];
-      load4(dx0 + (int64_t)perm[i] * D + c, u);
+      load4(dx0 + (int64_t)perm[i] * D + c0, u);
 #pragma unroll
       for (int j = 0; j < 4; ++j) s[j] += u[j];
     }
-    float* o = gtok + (int64_t)v * D + c;
-    if (beta) {
-      float ov[4];
-      load4(o, ov);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += ov[j];
-    }
-    store4(o, s);
+    for (int j = 0; j < 4; ++j) atomicAdd(gtok + (int64_t)cur * D + c0 + j, s[j]);
   }
 }
 
@@ -371,8 +421,8 @@ extern "C" int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int
   if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
   else LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
   CLIPMI_CHECK_LAUNCH();
-  if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
-  if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
+  if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
+  if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
@@ -397,7 +447,7 @@ extern "C" int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx
   dim3 g((N / 4 + 255) / 256, chunks);
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, R, N, rows_per, (float*)ws);
   else hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, R, N, rows_per, (float*)ws);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 255) / 256), dim3(256), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
@@ -424,8 +474,8 @@ extern "C" int clipmi_text_embed(void* stream, int dtype, const int64_t* ids, co
   return CLIPMI_OK;
 }
 
-// workspace (ints): counts[V] + offs[V+1] + cursor[V] + perm[R]
-extern "C" int64_t clipmi_text_embed_bwd_ws(int R, int V) { return ((int64_t)3 * V + 1 + R) * 4; }
+// workspace (ints): counts[V] + offs[V+1] + cursor[V] + perm[R] + sorted_id[R]
+extern "C" int64_t clipmi_text_embed_bwd_ws(int R, int V) { return ((int64_t)3 * V + 1 + 2 * (int64_t)R) * 4; }
 
 extern "C" int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids, const void* dx0, int R, int D, int V,
                                      float* gtok, int beta, void* ws, int64_t ws_bytes) {
@@ -436,12 +486,17 @@ extern "C" int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids
   int* offs = counts + V;
   int* cursor = offs + V + 1;
   int* perm = cursor + V;
+  int* sid = perm + R;
+  if (!beta) CLIPMI_HIP(hipMemsetAsync(gtok, 0, (size_t)V * D * 4, s));
   CLIPMI_HIP(hipMemsetAsync(counts, 0, (size_t)V * 4, s));
+  CLIPMI_HIP(hipMemsetAsync(sid, 0xff, (size_t)R * 4, s));
   hipLaunchKernelGGL(id_count_kernel, dim3((R + 255) / 256), dim3(256), 0, s, ids, R, V, counts);
   hipLaunchKernelGGL(id_scan_kernel, dim3(1), dim3(1024), 0, s, counts, V, offs, cursor);
-  hipLaunchKernelGGL(id_place_kernel, dim3((R + 255) / 256), dim3(256), 0, s, ids, R, V, cursor, perm);
-  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(id_segsum_kernel<bf16>, dim3((V + 3) / 4), dim3(256), 0, s, offs, perm, (const bf16*)dx0, D, V, gtok, beta);
-  else hipLaunchKernelGGL(id_segsum_kernel<float>, dim3((V + 3) / 4), dim3(256), 0, s, offs, perm, (const float*)dx0, D, V, gtok, beta);
+  hipLaunchKernelGGL(id_place_kernel, dim3((R + 255) / 256), dim3(256), 0, s, ids, R, V, cursor, perm, sid);
+  // rows with invalid ids were not placed: the sorted prefix has offs[V] entries
+  const int chunks = (R + 63) / 64;
+  if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(id_chunk_sum_kernel<bf16>, dim3((chunks + 3) / 4), dim3(256), 0, s, perm, sid, offs + V, (const bf16*)dx0, D, gtok);
+  else hipLaunchKernelGGL(id_chunk_sum_kernel<float>, dim3((chunks + 3) / 4), dim3(256), 0, s, perm, sid, offs + V, (const float*)dx0, D, gtok);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
