@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
-    ap.add_argument("--roofline-kernel", default="gemm_fwd_bias_qgelu_pre")
+    ap.add_argument("--roofline-kernel", default="gemm256_wgrad_splitk")
     ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     return ap.parse_args()

@@ -41,7 +41,7 @@ def test_invalid_args_raise_without_gpu():
     d.M, d.N, d.K = 16, 12, 64  # N % 8 != 0
     d.ab_dtype = d.c_dtype = 1
     st = _lib.lib().clipmi_gemm(None, ctypes.byref(d))
-    assert st == -1 and b"multiple of 8" in _lib.lib().clipmi_last_error()
+    assert st == -1 and b"N % 8" in _lib.lib().clipmi_last_error()
     with pytest.raises(ValueError):
         _lib.check(st, "clipmi_gemm")
 

@@ -320,6 +320,70 @@ __device__ __forceinline__ bf16x8 read_frag256(const char* img, int rb, int kk, 
   return read_frag<false>(img + (rb >> 7) * 16384, rb & 127, kk, lane);
 }
 
+// Batched epilogue for the 256 kernel (vectorisable case): bias preloaded once per lane,
+// residual / pre-activation / old-C vectors for half the tile loaded in one burst (clamped
+// addresses, no per-element branches), then computed and stored.  The per-subtile
+// load->wait->store chain it replaces left the K=768 GEMMs epilogue-latency bound.
+template <typename OutT, int EPI>
+__device__ __forceinline__ void epilogue256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
+  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
+  constexpr bool HAUX = HDQ || HDG;
+  const int nlane = (lane >> 4) * 4, mlane = lane & 15;
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = min(nb + j * 16 + nlane, p.N - 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) load4((const float*)p.bias + n, bv[j]);
+      else load4((const bf16*)p.bias + n, bv[j]);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float xin[4][4][4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = min(nb + j * 16 + nlane, p.N - 4);
+        if (HR) load4((const OutT*)p.res + (int64_t)m * p.ldr + n, xin[ii][j]);
+        else if (HAUX) load4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][j]);
+        else if (HBETA) load4((const OutT*)p.C + (int64_t)m * p.ldc + n, xin[ii][j]);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = h * 4 + ii;
+      const int m = mb + i * 16 + mlane;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + j * 16 + nlane;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r] * p.alpha + bv[j][r];
+        }
+        const bool ok = m < p.M && n < p.N;
+        if (HPRE && ok) store4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (HQ) v[r] = quick_gelu(v[r]);
+          if (HG) v[r] = gelu_erf(v[r]);
+          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][j][r]);
+          if (HDG) v[r] *= gelu_erf_grad(xin[ii][j][r]);
+          if (HR || HBETA) v[r] += xin[ii][j][r];
+        }
+        if (ok) store4((OutT*)p.C + (int64_t)m * p.ldc + n, v);
+      }
+    }
+  }
+}
+
 template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD>
 __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -393,6 +457,14 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       const int m = m0 + wm * 128 + i * 16 + lane;
       if (m < p.M) atomicAdd(bias_grad + m, accb[i][0]);
     }
+  }
+  // fast path: specialised epilogue, 4-aligned columns (N % 4 == 0) and aligned leading dims
+  // (residual+aux together never occur on this path)
+  constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
+                        !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
+  if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
+    epilogue256<OutT, EPI < 0 ? 0 : EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+    return;
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
