@@ -54,7 +54,7 @@ typedef struct clipmi_gemm_desc {
   int split_k;
   void* workspace; int64_t workspace_bytes;
   float* bias_grad;     /* wgrad only: bias_grad[m] += sum_k A(m,k) (fused Linear bias gradient, fp32) */
-  int force_small_tile; /* 1: use the 128x128 register-staged kernel (testing) */
+  int force_small_tile; /* 1: 128x128 register-staged kernel; >=2: 256-kernel schedule variant (bench) */
 } clipmi_gemm_desc;
 
 #define CLIPMI_EPI_BIAS 1

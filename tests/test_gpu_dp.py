@@ -1,0 +1,69 @@
+"""Data-parallel path with the real kernels: 2 ranks share cuda:0 over a gloo group
+(RCCL needs one GPU per rank; the driver's 8-GPU run exercises RCCL itself).  The sum of
+the ranks' losses and the all-reduced gradients must equal the single-device result on
+the same global batch, fp32 parity mode."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "vlm-clip_amd"))
+    import torch.distributed as dist
+    from clipmi import CLIPWithAdapters, synth
+    from clipmi.trainer import FusedAdamW
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = CLIPWithAdapters("tiny", use_text_adapter=True, use_vision_adapter=True, use_shared_adapters=False,
+                         freeze_clip=False, device="cuda:0", precision="fp32", pooling="eos",
+                         process_group=dist.group.WORLD)
+    B = 4
+    b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas())
+    opt.zero_grad()
+    out = m(**b)
+    out["loss"].backward()
+    opt.grads_all_reduce(dist.group.WORLD)
+    torch.cuda.synchronize()
+    g = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters() if p.grad is not None}
+    q.put((rank, out["loss"].item(), g))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_data_parallel_matches_single_device():
+    import torch.multiprocessing as mp
+    from clipmi import CLIPWithAdapters, synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 500
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(120)
+    m = CLIPWithAdapters("tiny", use_shared_adapters=False, freeze_clip=False, device="cuda:0", precision="fp32",
+                         pooling="eos")
+    b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, 8, seed=5).items()}
+    out = m(**b)
+    out["loss"].backward()
+    torch.cuda.synchronize()
+    ref = {n: p.grad.detach().cpu().numpy() for n, p in m.named_parameters() if p.grad is not None}
+    gmax = max(float(np.abs(r).max()) for r in ref.values())
+    for rank, loss, g in res:
+        assert abs(loss - out["loss"].item()) < 1e-5, (rank, loss, out["loss"].item())
+        worst = (0.0, "")
+        for n, r in ref.items():
+            # floor at 1 % of the largest gradient: some true gradients are ~0 (k biases)
+            scale = max(float(np.abs(r).max()), 1e-2 * gmax)
+            worst = max(worst, (float(np.abs(g[n] - r).max()) / scale, n))
+        assert worst[0] < 1e-4, worst

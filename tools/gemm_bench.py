@@ -18,6 +18,7 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("qkv_wgrad", 2304, 768, R, False, False, torch.float32, _lib.EPI_BETA, 2),
     ("out_wgrad", 768, 768, R, False, False, torch.float32, _lib.EPI_BETA, 8),
 ]
+VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,1").split(",")]
 only = sys.argv[1:] if len(sys.argv) > 1 else None
 torch.manual_seed(0)
 for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
@@ -38,8 +39,8 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,
               split_k=split, workspace=ws, bias_grad=bg)
-    for small in (False, True):
-        if small and bg is not None:
+    for small in VARIANTS:  # 0 = production schedule, 1 = 128 tile, 2 = up-front DMA issue
+        if small == 1 and bg is not None:
             kw2 = dict(kw, bias_grad=None)
         else:
             kw2 = kw
@@ -55,5 +56,5 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / n
-        print(f"{name:10s} {'128' if small else '256'} M={M} N={N} K={Kd} split={split}: {ms * 1e3:8.1f} us "
+        print(f"{name:10s} v{small} M={M} N={N} K={Kd} split={split}: {ms * 1e3:8.1f} us "
               f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)

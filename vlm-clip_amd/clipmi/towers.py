@@ -472,20 +472,39 @@ class PoolProjFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------ contrastive
+def _rccl(group):
+    return dist.get_backend(group) == "nccl"
+
+
 def _gather(x, group, world):
+    """All-gather rows over the group (RCCL all_gather_into_tensor; list form for gloo)."""
     if world == 1:
         return x
-    out = torch.empty(world * x.shape[0], *x.shape[1:], dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
-    return out
+    x = x.contiguous()
+    if _rccl(group):
+        out = torch.empty(world * x.shape[0], *x.shape[1:], dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=group)
+        return out
+    parts = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(parts, x, group=group)
+    return torch.cat(parts)
 
 
 def _reduce_scatter(x, group, world):
+    """Sum over the group, keep this rank's row block (RCCL reduce_scatter_tensor; gloo:
+    all_reduce + slice, which gloo supports for device tensors)."""
     if world == 1:
         return x
-    out = torch.empty(x.shape[0] // world, *x.shape[1:], dtype=x.dtype, device=x.device)
-    dist.reduce_scatter_tensor(out, x.contiguous(), group=group)
-    return out
+    x = x.contiguous()
+    n = x.shape[0] // world
+    if _rccl(group):
+        out = torch.empty(n, *x.shape[1:], dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x, group=group)
+        return out
+    y = x.clone()
+    dist.all_reduce(y, group=group)
+    r = dist.get_rank(group)
+    return y[r * n:(r + 1) * n].contiguous()
 
 
 class ContrastiveFn(torch.autograd.Function):

@@ -68,12 +68,14 @@ struct AttnP {
 };
 
 // ----------------------------------------------------------------------------- fwd
-template <int NKT, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p) {
+// MASKED = false: bidirectional, no key padding (vision) -> validity is key < N, tested only
+// in the boundary tile.  MASKED = true: key padding from LDS + optional causal (text).
+template <int NKT, bool MASKED>
+__global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p, int causal) {
   constexpr int NPAD = NKT * 16;
   __shared__ __attribute__((aligned(16))) char Kimg[NPAD * 128];
   __shared__ __attribute__((aligned(16))) char Vimg[NPAD * 128];
-  __shared__ int keyok[NPAD];
+  __shared__ int keyok[MASKED ? NPAD : 1];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
   const int N = p.N, D = p.D;
@@ -81,7 +83,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p) {
   const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
   stage_img(Kimg, base + D, ld, N, NPAD, t, 256);
   stage_img(Vimg, base + 2 * D, ld, N, NPAD, t, 256);
-  for (int k = t; k < NPAD; k += 256) keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+  if (MASKED)
+    for (int k = t; k < NPAD; k += 256) keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
   __syncthreads();
 
   const float c2 = p.scale * LOG2E;
@@ -101,27 +104,33 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p) {
       for (int kk = 0; kk < 2; ++kk)
         s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
     }
-    // s[kt][r] = score(q, key = kt*16 + 4g + r)
+    // s[kt][r] = raw score(q, key = kt*16 + 4g + r); invalid keys -> -inf
     float mx = NEG_INF;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (MASKED) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        bool ok = keyok[key] && (!CAUSAL || key <= q);
-        float v = ok ? s[kt][r] * c2 : NEG_INF;
-        s[kt][r] = v;
-        mx = fmaxf(mx, v);
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + 4 * g + r;
+          if (!(keyok[key] && (!causal || key <= q))) s[kt][r] = NEG_INF;
+        }
+      } else if (kt * 16 + 15 >= N) {  // boundary tile only
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + 4 * g + r >= N) s[kt][r] = NEG_INF;
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mref = mx == NEG_INF ? 0.f : mx;
+    const float mref = mx == NEG_INF ? 0.f : mx * c2;
     float l = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float e = exp2f(s[kt][r] - mref);
+        const float e = exp2f(fmaf(s[kt][r], c2, -mref));
         s[kt][r] = e;
         l += e;
       }
@@ -151,27 +160,34 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p) {
 }
 
 // ----------------------------------------------------------------------------- bwd
+// Two phases share one LDS region of two [Npad][64] images (~57 KiB at N=197), so two
+// 8-wave workgroups fit per CU and one's staging overlaps the other's MFMAs.
+//   phase A (dK, dV): LDS holds Q and dO; each wave owns 16 keys whose K/V fragments come
+//                     straight from global memory into registers.
+//   phase B (dQ):     LDS is restaged with K and V; each wave owns 16 queries whose Q/dO
+//                     fragments come from global memory.
+__device__ __forceinline__ bf16x8 gfrag(const bf16* rowbase, int64_t ld, int r, int N, int kk, int g) {
+  if (r >= N) return bf16x8{};  // padded rows contribute zero
+  return *(const bf16x8*)(rowbase + (int64_t)r * ld + kk * 32 + 8 * g);
+}
+
 template <bool CAUSAL>
-__global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
+__global__ __launch_bounds__(512, 4) void attn_bwd_mfma(AttnP p) {  // 2 WGs per CU = 4 waves per SIMD
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
   const int N = p.N, D = p.D;
   const int NPAD = (N + 31) & ~31;
   const int64_t ld = 3 * (int64_t)D;
-  char* Qimg = smem;
-  char* Kimg = smem + NPAD * 128;
-  char* Vimg = smem + 2 * NPAD * 128;
-  char* Oimg = smem + 3 * NPAD * 128;  // dO image
-  float* lse2 = (float*)(smem + 4 * NPAD * 128);
+  char* img0 = smem;                    // phase A: Q,  phase B: K
+  char* img1 = smem + NPAD * 128;       // phase A: dO, phase B: V
+  float* lse2 = (float*)(smem + 2 * NPAD * 128);
   float* delta = lse2 + NPAD;
   int* keyok = (int*)(delta + NPAD);
   const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
   const bf16* dob = p.dout + (int64_t)b * N * D + h * 64;
-  stage_img(Qimg, base, ld, N, NPAD, t, 512);
-  stage_img(Kimg, base + D, ld, N, NPAD, t, 512);
-  stage_img(Vimg, base + 2 * D, ld, N, NPAD, t, 512);
-  stage_img(Oimg, dob, D, N, NPAD, t, 512);
+  stage_img(img0, base, ld, N, NPAD, t, 512);
+  stage_img(img1, dob, D, N, NPAD, t, 512);
   // delta[q] = sum_d dO*O ; 8 lanes per row
   {
     const bf16* ob = p.o + (int64_t)b * N * D + h * 64;
@@ -203,15 +219,15 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
   const int g = lane >> 4, li = lane & 15;
   const int nkb = NPAD >> 4, nstep = NPAD >> 5;
 
-  // ---- phase A: dK, dV for 16 keys per wave
+  // ---- phase A: dK, dV for 16 keys per wave (Q image in img0, dO image in img1)
   for (int kb = wave; kb < nkb; kb += 8) {
-    const int key = kb * 16 + li;  // this lane's key (column of the score tiles)
+    const int key = kb * 16 + li;
     const bool kok = keyok[key];
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      kf[kk] = frag_row(Kimg, kb * 16 + li, kk * 4 + g);
-      vf[kk] = frag_row(Vimg, kb * 16 + li, kk * 4 + g);
+      kf[kk] = gfrag(base + D, ld, key, N, kk, g);
+      vf[kk] = gfrag(base + 2 * D, ld, key, N, kk, g);
     }
     f32x4 dv[4], dk[4];
 #pragma unroll
@@ -221,19 +237,18 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
       f32x4 pt[2], ds[2];
 #pragma unroll
       for (int tau = 0; tau < 2; ++tau) {
-        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = s;
+        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
         const int qr = qs * 32 + tau * 16 + li;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Qimg, qr, kk * 4 + g), kf[kk], s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Oimg, qr, kk * 4 + g), vf[kk], dp, 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img0, qr, kk * 4 + g), kf[kk], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img1, qr, kk * 4 + g), vf[kk], dp, 0, 0, 0);
         }
-        // s[r] = score(q = qs*32 + tau*16 + 4g + r, key)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = qs * 32 + tau * 16 + 4 * g + r;
           const bool ok = kok && (!CAUSAL || key <= q);
-          const float pv = ok ? exp2f(s[r] * c2 - lse2[q]) : 0.f;
+          const float pv = ok ? exp2f(sc[r] * c2 - lse2[q]) : 0.f;
           pt[tau][r] = pv;
           ds[tau][r] = pv * (dp[r] - delta[q]);
         }
@@ -242,8 +257,8 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
       const bf16x8 sf = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        dv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Oimg, qs * 32, u * 16, lane), pf, dv[u], 0, 0, 0);
-        dk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Qimg, qs * 32, u * 16, lane), sf, dk[u], 0, 0, 0);
+        dv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img1, qs * 32, u * 16, lane), pf, dv[u], 0, 0, 0);
+        dk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img0, qs * 32, u * 16, lane), sf, dk[u], 0, 0, 0);
       }
     }
     if (key < N) {
@@ -257,8 +272,12 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
       }
     }
   }
+  __syncthreads();
+  stage_img(img0, base + D, ld, N, NPAD, t, 512);
+  stage_img(img1, base + 2 * D, ld, N, NPAD, t, 512);
+  __syncthreads();
 
-  // ---- phase B: dQ for 16 queries per wave
+  // ---- phase B: dQ for 16 queries per wave (K image in img0, V image in img1)
   const int nqb = (N + 15) >> 4;
   for (int qb = wave; qb < nqb; qb += 8) {
     const int q = qb * 16 + li;
@@ -266,8 +285,8 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
     bf16x8 qf[2], of[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      qf[kk] = frag_row(Qimg, q, kk * 4 + g);
-      of[kk] = frag_row(Oimg, q, kk * 4 + g);
+      qf[kk] = gfrag(base, ld, q, N, kk, g);
+      of[kk] = gfrag(dob, D, q, N, kk, g);
     }
     f32x4 dq[4];
 #pragma unroll
@@ -277,26 +296,25 @@ __global__ __launch_bounds__(512) void attn_bwd_mfma(AttnP p) {
       f32x4 ds[2];
 #pragma unroll
       for (int tau = 0; tau < 2; ++tau) {
-        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = s;
+        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
         const int kr = ks * 32 + tau * 16 + li;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kr, kk * 4 + g), qf[kk], s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Vimg, kr, kk * 4 + g), of[kk], dp, 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img0, kr, kk * 4 + g), qf[kk], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img1, kr, kk * 4 + g), of[kk], dp, 0, 0, 0);
         }
-        // s[r] = score(q, key = ks*32 + tau*16 + 4g + r)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = ks * 32 + tau * 16 + 4 * g + r;
           const bool ok = keyok[key] && (!CAUSAL || key <= q);
-          const float pv = ok ? exp2f(s[r] * c2 - l2) : 0.f;
+          const float pv = ok ? exp2f(sc[r] * c2 - l2) : 0.f;
           ds[tau][r] = pv * (dp[r] - dl);
         }
       }
       const bf16x8 sf = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        dq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Kimg, ks * 32, u * 16, lane), sf, dq[u], 0, 0, 0);
+        dq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img0, ks * 32, u * 16, lane), sf, dq[u], 0, 0, 0);
     }
     if (q < N) {
       bf16* row = p.dqkv + ((int64_t)b * N + q) * ld + h * 64;
@@ -455,19 +473,19 @@ __global__ __launch_bounds__(1024) void attn_bwd_f32(AttnF p) {
   }
 }
 
-template <bool C>
-int fwd_dispatch(const AttnP& p, hipStream_t s) {
+template <bool M>
+int fwd_dispatch(const AttnP& p, int causal, hipStream_t s) {
   const int nkt = ((p.N + 31) & ~31) / 16;
   const dim3 g(p.B * p.H), blk(256);
   switch (nkt) {
-    case 2: hipLaunchKernelGGL((attn_fwd_mfma<2, C>), g, blk, 0, s, p); break;
-    case 4: hipLaunchKernelGGL((attn_fwd_mfma<4, C>), g, blk, 0, s, p); break;
-    case 6: hipLaunchKernelGGL((attn_fwd_mfma<6, C>), g, blk, 0, s, p); break;
-    case 8: hipLaunchKernelGGL((attn_fwd_mfma<8, C>), g, blk, 0, s, p); break;
-    case 10: hipLaunchKernelGGL((attn_fwd_mfma<10, C>), g, blk, 0, s, p); break;
-    case 12: hipLaunchKernelGGL((attn_fwd_mfma<12, C>), g, blk, 0, s, p); break;
-    case 14: hipLaunchKernelGGL((attn_fwd_mfma<14, C>), g, blk, 0, s, p); break;
-    case 16: hipLaunchKernelGGL((attn_fwd_mfma<16, C>), g, blk, 0, s, p); break;
+    case 2: hipLaunchKernelGGL((attn_fwd_mfma<2, M>), g, blk, 0, s, p, causal); break;
+    case 4: hipLaunchKernelGGL((attn_fwd_mfma<4, M>), g, blk, 0, s, p, causal); break;
+    case 6: hipLaunchKernelGGL((attn_fwd_mfma<6, M>), g, blk, 0, s, p, causal); break;
+    case 8: hipLaunchKernelGGL((attn_fwd_mfma<8, M>), g, blk, 0, s, p, causal); break;
+    case 10: hipLaunchKernelGGL((attn_fwd_mfma<10, M>), g, blk, 0, s, p, causal); break;
+    case 12: hipLaunchKernelGGL((attn_fwd_mfma<12, M>), g, blk, 0, s, p, causal); break;
+    case 14: hipLaunchKernelGGL((attn_fwd_mfma<14, M>), g, blk, 0, s, p, causal); break;
+    case 16: hipLaunchKernelGGL((attn_fwd_mfma<16, M>), g, blk, 0, s, p, causal); break;
     default: return clipmi_invalid("attention: N must be <= 256");
   }
   return CLIPMI_OK;
@@ -488,7 +506,7 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
     ProfScope ps(s, "attn_fwd", flops);
-    CLIPMI_TRY(causal ? fwd_dispatch<true>(p, s) : fwd_dispatch<false>(p, s));
+    CLIPMI_TRY((causal || attention_mask) ? fwd_dispatch<true>(p, causal, s) : fwd_dispatch<false>(p, causal, s));
     ps.finish("attn_fwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, causal, 0.125f};
@@ -514,7 +532,7 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
     const int npad = (N + 31) & ~31;
-    size_t lds = (size_t)npad * 128 * 4 + (size_t)npad * 12;
+    size_t lds = (size_t)npad * 128 * 2 + (size_t)npad * 12;
     static bool attr = false;
     if (!attr) {
       CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

@@ -42,6 +42,7 @@ struct GemmP {
   int k_per_split; float* ws;
   int tiles_n, ntiles;
   int vec;  // all leading dimensions multiples of 4 elements
+  int var;  // 256-kernel main-loop schedule (0 production)
 };
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
@@ -314,6 +315,36 @@ __device__ __forceinline__ void stage256(char* img, const bf16* X, int64_t ld, i
   }
 }
 
+// issue DMA instruction i (0..3) of this wave for one operand tile (same addressing as stage256)
+template <bool KMAJ>
+__device__ __forceinline__ void stage256_one(char* img, __amdgpu_buffer_rsrc_t rs, int64_t ld, int wave, int lane, int i) {
+  const int j = wave * 4 + i;
+  if (KMAJ) {
+    const int r = 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    dma16(rs, img + j * 1024, (int)((int64_t)r * ld * 2 + c * 16));
+  } else {
+    const int half = j >> 4;
+    const int kr = 4 * (j & 15) + (lane >> 4);
+    const int c = (lane & 15) ^ mimg_swz(kr);
+    dma16(rs, img + half * 16384 + (j & 15) * 1024, (int)((int64_t)kr * ld * 2 + (half * 128 + c * 8) * 2));
+  }
+}
+template <bool KMAJ>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
+  if (KMAJ) {
+    const int rows = min(BT, R - row0);
+    const bf16* base = X + (int64_t)row0 * ld + k0;
+    const uint32_t rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+  }
+  const int krows = min(64, K - k0);
+  const int cols = min(BT, R - row0);
+  const bf16* base = X + (int64_t)k0 * ld + row0;
+  const uint32_t rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+}
+
 template <bool KMAJ>
 __device__ __forceinline__ bf16x8 read_frag256(const char* img, int rb, int kk, int lane) {
   if (KMAJ) return read_frag<true>(img, rb, kk, lane);
@@ -384,7 +415,7 @@ __device__ __forceinline__ void epilogue256(const GemmP& p, f32x4 (&acc)[8][4], 
   }
 }
 
-template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD>
+template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD, int VAR = 0>
 __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
@@ -423,10 +454,16 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
   __syncthreads();
   for (int it = 0; it < nk; ++it) {
     const int cur = it & 1;
-    if (it + 1 < nk) {
-      const int k1 = kbeg + (it + 1) * BK;
+    const bool more = it + 1 < nk;
+    const int k1 = kbeg + (it + 1) * BK;
+    if (VAR == 0 && more) {
       stage256<AK>(IMG_A(cur ^ 1), A, p.lda, m0, p.M, k1, Kv, wave, lane);
       stage256<BKM>(IMG_B(cur ^ 1), B, p.ldb, n0, p.N, k1, Kv, wave, lane);
+    }
+    __amdgpu_buffer_rsrc_t ra, rb;
+    if (VAR != 0) {
+      ra = rsrc256<AK>(A, p.lda, m0, p.M, more ? k1 : kbeg, Kv);
+      rb = rsrc256<BKM>(B, p.ldb, n0, p.N, more ? k1 : kbeg, Kv);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -435,15 +472,22 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       for (int i = 0; i < 8; ++i) fa[i] = read_frag256<AK>(IMG_A(cur), wm * 128 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = read_frag256<BKM>(IMG_B(cur), wn * 64 + j * 16, kk, lane);
+      if (VAR == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i) {
+        if (VAR != 0 && kk == 0 && more) {  // one DMA per 4 MFMAs across the first half of the step
+          if (i < 4) stage256_one<AK>(IMG_A(cur ^ 1), ra, p.lda, wave, lane, i);
+          else stage256_one<BKM>(IMG_B(cur ^ 1), rb, p.ldb, wave, lane, i - 4);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
       if (BIASGRAD && do_bias) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fa[i], accb[i], 0, 0, 0);
       }
+      if (VAR == 2) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -555,16 +599,25 @@ void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT, EPI>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
 }
 
-template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
-void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, int VAR>
+void launch256v(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   static bool attr = false;  // 128 KiB of dynamic LDS needs the opt-in once per instance
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, OutT, EPI, BG>,
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG>), dim3(p.ntiles, splits), dim3(NT2), 131072, s, p,
-                     bias_grad);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>), dim3(p.ntiles, splits), dim3(NT2), 131072, s,
+                     p, bias_grad);
+}
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
+  // main-loop schedule: VAR 2 (DMA issue interleaved with the MFMA stream + s_setprio around
+  // the MFMA clusters) is production; 0 (all DMAs issued up front) kept for A/B runs.
+  switch (p.var) {
+    case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
+    default: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
+  }
 }
 
 constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU, E_G = CLIPMI_EPI_GELU;
@@ -677,12 +730,13 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
   p.bias_f32 = d->bias_dtype == CLIPMI_F32;
   p.ws = nullptr;
+  p.var = d->force_small_tile >= 2 ? d->force_small_tile : 0;
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
           ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
   // 256x256 LDS-DMA kernel for the big shapes (k-major operands need K % 64 == 0: the
   // buffer range check zero-fills rows, not a row's k tail)
   const bool kok = (!d->a_kmajor || d->K % 64 == 0) && (!d->b_kmajor || d->K % 64 == 0);
-  const bool use256 = bf && kok && ((d->M >= 256 && d->N >= 128) || d->bias_grad) && !d->force_small_tile;
+  const bool use256 = bf && kok && ((d->M >= 256 && d->N >= 128) || d->bias_grad) && d->force_small_tile != 1;
   CLIPMI_REQUIRE(!d->bias_grad || use256, "bias_grad fusion needs the 256 kernel (bf16, wgrad layout)");
   const int tile = bf ? (use256 ? BT : BM) : FT;
   const int kstep = bf ? BK : FK;
