@@ -39,6 +39,21 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,
               split_k=split, workspace=ws, bias_grad=bg)
+    if os.environ.get("GEMM_TORCH"):  # hipBLASLt via torch.matmul, plain product, for comparison
+        a2 = A.view(M, Kd) if akm else A.view(Kd, M).t()
+        b2 = B.view(N, Kd).t() if bkm else B.view(Kd, N)
+        g = lambda: torch.matmul(a2, b2)
+        for _ in range(3):
+            g()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(10):
+            g()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 10
+        print(f"{name:10s} torch M={M} N={N} K={Kd}: {ms * 1e3:8.1f} us {2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
     for small in VARIANTS:  # 0 = production schedule, 1 = 128 tile, 2 = up-front DMA issue
         if small == 1 and bg is not None:
             kw2 = dict(kw, bias_grad=None)

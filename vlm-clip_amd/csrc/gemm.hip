@@ -26,6 +26,7 @@
 #include "common.h"
 #include "internal.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 
@@ -279,6 +280,25 @@ constexpr int BT = 256, NT2 = 512;
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, int voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0, 0);
 }
+// The same DMA issued from inline asm.  hipcc's waitcnt pass treats every
+// ds_read_b64_tr_b16 as aliasing any LDS-DMA it can see and puts s_waitcnt vmcnt(0) in
+// front of it, which drains the next k-step's prefetch in the middle of the current one;
+// DMAs it cannot see are ordered by this kernel's own vmcnt + barrier instead.
+struct SRsrc { u32x4 v; };
+__device__ __forceinline__ SRsrc make_srsrc(const void* base, uint32_t num_records) {
+  const uint64_t b = (uint64_t)base;
+  SRsrc r;
+  r.v[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r.v[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xffffu);
+  r.v[2] = __builtin_amdgcn_readfirstlane(num_records);
+  r.v[3] = 0x00020000u;
+  return r;
+}
+__device__ __forceinline__ void dma16(SRsrc r, char* lds_wave_base, int voff) {
+  const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r.v)
+               : "memory");
+}
 
 // stage one 256x64 operand tile of k-step at k0 into an LDS image (32 KiB)
 template <bool KMAJ>
@@ -316,8 +336,8 @@ __device__ __forceinline__ void stage256(char* img, const bf16* X, int64_t ld, i
 }
 
 // issue DMA instruction i (0..3) of this wave for one operand tile (same addressing as stage256)
-template <bool KMAJ>
-__device__ __forceinline__ void stage256_one(char* img, __amdgpu_buffer_rsrc_t rs, int64_t ld, int wave, int lane, int i) {
+template <bool KMAJ, typename RS>
+__device__ __forceinline__ void stage256_one(char* img, RS rs, int64_t ld, int wave, int lane, int i) {
   const int j = wave * 4 + i;
   if (KMAJ) {
     const int r = 8 * j + (lane >> 3);
@@ -331,18 +351,30 @@ __device__ __forceinline__ void stage256_one(char* img, __amdgpu_buffer_rsrc_t r
   }
 }
 template <bool KMAJ>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
+__device__ __forceinline__ void extent256(const bf16* X, int64_t ld, int row0, int R, int k0, int K, const bf16*& base,
+                                          uint32_t& rec) {
   if (KMAJ) {
     const int rows = min(BT, R - row0);
-    const bf16* base = X + (int64_t)row0 * ld + k0;
-    const uint32_t rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+    base = X + (int64_t)row0 * ld + k0;
+    rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
+  } else {
+    const int krows = min(64, K - k0);
+    const int cols = min(BT, R - row0);
+    base = X + (int64_t)k0 * ld + row0;
+    rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
   }
-  const int krows = min(64, K - k0);
-  const int cols = min(BT, R - row0);
-  const bf16* base = X + (int64_t)k0 * ld + row0;
-  const uint32_t rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
+}
+template <bool KMAJ>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
+  const bf16* base; uint32_t rec;
+  extent256<KMAJ>(X, ld, row0, R, k0, K, base, rec);
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
+}
+template <bool KMAJ>
+__device__ __forceinline__ SRsrc srsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
+  const bf16* base; uint32_t rec;
+  extent256<KMAJ>(X, ld, row0, R, k0, K, base, rec);
+  return make_srsrc(base, rec);
 }
 
 template <bool KMAJ>
@@ -447,8 +479,17 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
 #define IMG_A(b) (smem + (b) * 65536)
 #define IMG_B(b) (smem + (b) * 65536 + 32768)
   if (nk > 0) {
-    stage256<AK>(IMG_A(0), A, p.lda, m0, p.M, kbeg, Kv, wave, lane);
-    stage256<BKM>(IMG_B(0), B, p.ldb, n0, p.N, kbeg, Kv, wave, lane);
+    if constexpr (VAR == 3) {
+      const SRsrc ra = srsrc256<AK>(A, p.lda, m0, p.M, kbeg, Kv), rb = srsrc256<BKM>(B, p.ldb, n0, p.N, kbeg, Kv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        stage256_one<AK>(IMG_A(0), ra, p.lda, wave, lane, i);
+        stage256_one<BKM>(IMG_B(0), rb, p.ldb, wave, lane, i);
+      }
+    } else {
+      stage256<AK>(IMG_A(0), A, p.lda, m0, p.M, kbeg, Kv, wave, lane);
+      stage256<BKM>(IMG_B(0), B, p.ldb, n0, p.N, kbeg, Kv, wave, lane);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -460,8 +501,12 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       stage256<AK>(IMG_A(cur ^ 1), A, p.lda, m0, p.M, k1, Kv, wave, lane);
       stage256<BKM>(IMG_B(cur ^ 1), B, p.ldb, n0, p.N, k1, Kv, wave, lane);
     }
-    __amdgpu_buffer_rsrc_t ra, rb;
-    if (VAR != 0) {
+    typedef typename std::conditional<VAR == 3, SRsrc, __amdgpu_buffer_rsrc_t>::type RS;
+    RS ra, rb;
+    if constexpr (VAR == 3) {
+      ra = srsrc256<AK>(A, p.lda, m0, p.M, more ? k1 : kbeg, Kv);
+      rb = srsrc256<BKM>(B, p.ldb, n0, p.N, more ? k1 : kbeg, Kv);
+    } else if constexpr (VAR != 0) {
       ra = rsrc256<AK>(A, p.lda, m0, p.M, more ? k1 : kbeg, Kv);
       rb = rsrc256<BKM>(B, p.ldb, n0, p.N, more ? k1 : kbeg, Kv);
     }
@@ -472,7 +517,7 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       for (int i = 0; i < 8; ++i) fa[i] = read_frag256<AK>(IMG_A(cur), wm * 128 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = read_frag256<BKM>(IMG_B(cur), wn * 64 + j * 16, kk, lane);
-      if (VAR == 2) __builtin_amdgcn_s_setprio(1);
+      if (VAR >= 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if (VAR != 0 && kk == 0 && more) {  // one DMA per 4 MFMAs across the first half of the step
@@ -487,7 +532,7 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
 #pragma unroll
         for (int i = 0; i < 8; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fa[i], accb[i], 0, 0, 0);
       }
-      if (VAR == 2) __builtin_amdgcn_s_setprio(0);
+      if (VAR >= 2) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -612,11 +657,13 @@ void launch256v(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
 }
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
 void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  // main-loop schedule: VAR 2 (DMA issue interleaved with the MFMA stream + s_setprio around
-  // the MFMA clusters) is production; 0 (all DMAs issued up front) kept for A/B runs.
+  // main-loop schedule: VAR 3 (DMA issue interleaved with the MFMA stream, s_setprio around
+  // the MFMA clusters, DMAs from inline asm) is production; var 2 -> VAR 0 (all DMAs issued
+  // up front), var 3 -> VAR 2 (builtin DMAs) kept for A/B runs.
   switch (p.var) {
     case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
-    default: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
+    case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
+    default: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
   }
 }
 
