@@ -36,9 +36,10 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("akm,bkm", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("small", [0, 1, 4])  # production (ping-pong 256), 128 tile, single-group 256
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 136, 72), (77, 64, 768), (1000, 512, 200),
-                                   (1000, 776, 768), (600, 264, 1000), (512, 256, 64)])
+                                   (1000, 776, 768), (600, 264, 1000), (512, 256, 64), (520, 384, 96),
+                                   (768, 256, 4160)])
 def test_gemm_layouts(dtype, akm, bkm, M, N, K, small):
     if dtype == torch.float32 and small:
         pytest.skip("tile choice only applies to the bf16 path")
@@ -102,7 +103,7 @@ def test_gemm_splitk_wgrad(dtype):
 
 
 @pytest.mark.parametrize("T,Nout,Kin,split", [(3000, 256, 192, 8), (50000, 768, 3072, 12), (77, 64, 128, 1),
-                                              (20000, 2304, 768, 4)])
+                                              (20000, 2304, 768, 4), (300, 768, 768, 3), (4100, 512, 256, 2)])
 def test_wgrad_fused_bias_grad(T, Nout, Kin, split):
     """256 wgrad kernel with the fused bias gradient (sum over tokens of dY)."""
     dY = _mk((T, Nout), torch.bfloat16, 12)

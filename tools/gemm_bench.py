@@ -17,12 +17,16 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("fc2_wgrad", 768, 3072, R, False, False, torch.float32, _lib.EPI_BETA, 2),
     ("qkv_wgrad", 2304, 768, R, False, False, torch.float32, _lib.EPI_BETA, 2),
     ("out_wgrad", 768, 768, R, False, False, torch.float32, _lib.EPI_BETA, 8),
+    # reference points (not on the CLIP path): square, operands resident in MALL
+    ("sq4k", 4096, 4096, 4096, True, True, torch.bfloat16, 0, 1),
+    ("sq8k", 8192, 8192, 8192, True, True, torch.bfloat16, 0, 1),
+    ("fc2_fwd_l2", 16384, 768, 3072, True, True, torch.bfloat16, 0, 1),
 ]
 VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,1").split(",")]
 only = sys.argv[1:] if len(sys.argv) > 1 else None
 torch.manual_seed(0)
 for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
-    if only and name not in only:
+    if (only and name not in only) or (not only and name in ("sq4k", "sq8k", "fc2_fwd_l2")):
         continue
     A = torch.randn(M * Kd, device="cuda").to(torch.bfloat16)
     B = torch.randn(N * Kd, device="cuda").to(torch.bfloat16)

@@ -27,6 +27,7 @@
 #include "internal.h"
 #include <algorithm>
 #include <type_traits>
+#include <cstdlib>
 
 namespace {
 
@@ -447,6 +448,32 @@ __device__ __forceinline__ void epilogue256(const GemmP& p, f32x4 (&acc)[8][4], 
   }
 }
 
+// Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
+// allows it (4-aligned columns, aligned leading dims), else the per-subtile generic path
+// (split-K slabs, ragged N, runtime flags).
+template <typename OutT, int EPI>
+__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+  constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
+                        !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
+  if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
+    epilogue256<OutT, EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mb + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nb + j * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
+      else epilogue4<OutT, EPI>(p, m, n, v);
+    }
+  }
+}
+
 template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD, int VAR = 0>
 __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -547,27 +574,181 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       if (m < p.M) atomicAdd(bias_grad + m, accb[i][0]);
     }
   }
-  // fast path: specialised epilogue, 4-aligned columns (N % 4 == 0) and aligned leading dims
-  // (residual+aux together never occur on this path)
-  constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
-                        !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
-  if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
-    epilogue256<OutT, EPI < 0 ? 0 : EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
-    return;
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+}
+
+// ------------------------------------------------------------------ ping-pong 256x256 path
+// Same 256x256 tile and 8-wave (2 along M x 4 along N) decomposition as gemm256_kernel, with
+// a schedule built so the matrix cores never wait on LDS or on the DMA queue:
+//  * k advances in stages of 32 through a ring of PP_S = 5 LDS stages (5 x 32 KiB = all
+//    160 KiB); stage s + PP_D is DMA'd while stage s is consumed (PP_D = 3 stages of
+//    prefetch, ~1.5 k-steps of the old schedule), waited for with a counted vmcnt, never 0.
+//  * each stage is two phases of 16 MFMAs per wave (m-half 0 / 1 of the wave's 128 rows x
+//    all 64 columns, k 32).  A phase is [load section: its fragments from LDS + 2 DMA issues
+//    (+ the counted wait)] barrier [MFMA section] barrier.
+//  * the 4 waves of M-half 1 start one barrier late, so on every SIMD (waves w and w + 4 share
+//    one) one wave runs its MFMA section while the other runs its load section: the two
+//    groups ping-pong between the matrix core and the LDS/DMA path.
+// Ring safety (intervals = spans between barriers; group 0's phase q is intervals 2q (load)
+// and 2q + 1 (MFMA), group 1's is 2q + 1 and 2q + 2): stage s + 3 is DMA'd in phases 2s, 2s + 1
+// into the slot of stage s - 2, whose last reads (group 1, phase 2s - 3, interval 4s - 5) were
+// retired by that group's lgkmcnt wait two intervals before the first overwrite (interval 4s).
+// Stage s + 1 is waited for (vmcnt) in both groups' load sections of phase 2s + 1, before the
+// barrier that precedes its first read (group 0, phase 2s + 2).
+// LDS images per stage: A at +0, B at +16 KiB.  k-major operand: [256 rows][32 k] = 64-B rows,
+// 16-B chunk c of row r at c ^ ((r >> 1) & 3); k-row operand: two [32 k][128] halves of 256-B
+// rows with gemm128's mimg swizzle.  Both conflict-free (tools/lds_banks.py).
+constexpr int PP_S = 5, PP_D = 3, PP_STAGE = 32768;
+
+__device__ __forceinline__ int kimg32_off(int r, int c) { return r * 64 + ((c ^ (r >> 1)) & 3) * 16; }
+
+// Two DMA wave-instructions (i = 0, 1) of this wave for one operand of one stage.
+template <bool KMAJ>
+__device__ __forceinline__ void stage_pp(char* img, const bf16* X, int64_t ld, int row0, int R, int k0, int K,
+                                         int wave, int lane) {
+  const bf16* base;
+  uint32_t rec;
+  if (KMAJ) {
+    const int rows = min(BT, R - row0);
+    base = X + (int64_t)row0 * ld + k0;
+    rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 64) : 0u;
+  } else {
+    const int krows = min(32, K - k0);
+    const int cols = min(BT, R - row0);
+    base = X + (int64_t)k0 * ld + row0;
+    rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
   }
+  const SRsrc rs = make_srsrc(base, rec);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
-      if (n >= p.N) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
-      else epilogue4<OutT, EPI>(p, m, n, v);
+  for (int i = 0; i < 2; ++i) {
+    const int j = wave * 2 + i;  // 0..15, 1 KiB each
+    if (KMAJ) {
+      const int r = 16 * j + (lane >> 2);
+      const int c = (lane & 3) ^ ((r >> 1) & 3);
+      dma16(rs, img + j * 1024, (int)((int64_t)r * ld * 2 + c * 16));
+    } else {
+      const int half = j >> 3;
+      const int kr = 4 * (j & 7) + (lane >> 4);
+      const int c = (lane & 15) ^ mimg_swz(kr);
+      dma16(rs, img + half * 8192 + (j & 7) * 1024, (int)((int64_t)kr * ld * 2 + (half * 128 + c * 8) * 2));
     }
   }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 read_frag_pp(const char* img, int rb, int lane) {
+  if (KMAJ) return *LDS_PTR(const bf16x8, img + kimg32_off(rb + (lane & 15), lane >> 4));
+  return read_frag<false>(img + (rb >> 7) * 8192, rb & 127, 0, lane);
+}
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// wait until at most n of this wave's DMAs are outstanding (n even, 0..8)
+__device__ __forceinline__ void pp_vmcnt(int n) {
+  switch (n) {
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// PPV (schedule experiments, 0 = production): bit 0 one phase of 32 MFMAs per stage instead
+// of two of 16; bit 1 no ping-pong (both groups in lock-step); bit 2 no s_setprio.
+template <bool AK, bool BKM, typename OutT, int EPI, bool BIASGRAD, int PPV = 0>
+__global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_grad) {
+  constexpr int NPH = (PPV & 1) ? 1 : 2, MPH = 8 / NPH;
+  constexpr bool PINGPONG = !(PPV & 2);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tile = xcd_remap(blockIdx.x, p.ntiles);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int ns = (kend - kbeg + 31) / 32;
+  const bf16* A = (const bf16*)p.A;
+  const bf16* B = (const bf16*)p.B;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient (wgrad, n-tile 0): wave wn sums m-fragments wn and 4 + wn
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const bool do_bias = BIASGRAD && tn == 0;
+  const bf16x8 ones = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+
+  auto slot = [&](int st) { return smem + (st % PP_S) * PP_STAGE; };
+  // prologue: stages 0 .. PP_D - 1
+#pragma unroll
+  for (int st = 0; st < PP_D; ++st) {
+    if (st < ns) {
+      stage_pp<AK>(slot(st), A, p.lda, m0, p.M, kbeg + st * 32, kend, wave, lane);
+      stage_pp<BKM>(slot(st) + 16384, B, p.ldb, n0, p.N, kbeg + st * 32, kend, wave, lane);
+    }
+  }
+  pp_vmcnt(4 * (min(PP_D, ns) - 1));  // stage 0 landed
+  pp_barrier();
+  if (PINGPONG && wm == 1) pp_barrier();
+
+  for (int st = 0; st < ns; ++st) {
+    const char* img = slot(st);
+    const bool issue = st + PP_D < ns;
+    const int kn = kbeg + (st + PP_D) * 32;
+    bf16x8 fb[4];  // the stage's B fragments, read in the first phase
+#pragma unroll
+    for (int ph = 0; ph < NPH; ++ph) {
+      // ---- load section
+      bf16x8 fa[MPH];
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = read_frag_pp<BKM>(img + 16384, wn * 64 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < MPH; ++i) fa[i] = read_frag_pp<AK>(img, wm * 128 + (ph * MPH + i) * 16, lane);
+      if (issue) {
+        if (NPH == 1 || ph == 0) stage_pp<AK>(slot(st + PP_D), A, p.lda, m0, p.M, kn, kend, wave, lane);
+        if (NPH == 1 || ph == 1) stage_pp<BKM>(slot(st + PP_D) + 16384, B, p.ldb, n0, p.N, kn, kend, wave, lane);
+      }
+      if (ph == NPH - 1) pp_vmcnt(4 * max(0, min(PP_D - 1, ns - st - 2)));  // stage st + 1 landed
+      pp_barrier();
+      // ---- MFMA section
+      if (!(PPV & 4)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MPH; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ph * MPH + i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[ph * MPH + i][j], 0, 0, 0);
+      if (BIASGRAD && do_bias) {
+#pragma unroll
+        for (int h = 0; h < MPH / 4; ++h) {
+          const bf16x8 f = wn == 0 ? fa[h * 4] : wn == 1 ? fa[h * 4 + 1] : wn == 2 ? fa[h * 4 + 2] : fa[h * 4 + 3];
+          accb[ph + h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, accb[ph + h], 0, 0, 0);
+        }
+      }
+      if (!(PPV & 4)) __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (PINGPONG && wm == 0) pp_barrier();  // pairs with group 1's leading barrier
+
+  if (BIASGRAD && do_bias && lane < 16) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+      const int m = m0 + wm * 128 + (mh * 4 + wn) * 16 + lane;
+      if (m < p.M) atomicAdd(bias_grad + m, accb[mh][0]);
+    }
+  }
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
 }
 
 // ------------------------------------------------------------------ f32 SIMT path
@@ -655,15 +836,33 @@ void launch256v(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>), dim3(p.ntiles, splits), dim3(NT2), 131072, s,
                      p, bias_grad);
 }
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, int PPV>
+void launch_ppv(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
+  static bool attr = false;  // the 5-stage ring takes all 160 KiB of LDS
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_S * PP_STAGE);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>), dim3(p.ntiles, splits), dim3(NT2),
+                     PP_S * PP_STAGE, s, p, bias_grad);
+}
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
 void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  // main-loop schedule: VAR 3 (DMA issue interleaved with the MFMA stream, s_setprio around
-  // the MFMA clusters, DMAs from inline asm) is production; var 2 -> VAR 0 (all DMAs issued
-  // up front), var 3 -> VAR 2 (builtin DMAs) kept for A/B runs.
+  // var 0 / 9: the ping-pong kernel; 4: gemm256_kernel VAR 3 (interleaved asm DMAs, the wgrad
+  // production schedule); 2 -> VAR 0 (all DMAs up front), 3 -> VAR 2 (builtin DMAs) for A/B.
   switch (p.var) {
     case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
     case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
-    default: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
+    case 4: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
+    case 9: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
+#ifdef CLIPMI_GEMM_EXPERIMENTS
+    case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
+    case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
+    case 7: launch_ppv<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
+    case 8: launch_ppv<AK, BKM, OutT, EPI, BG, 4>(p, splits, s, bias_grad); break;
+#endif
+    default: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
   }
 }
 
@@ -777,7 +976,16 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
   p.bias_f32 = d->bias_dtype == CLIPMI_F32;
   p.ws = nullptr;
-  p.var = d->force_small_tile >= 2 ? d->force_small_tile : 0;
+  // 256-kernel schedule: the ping-pong kernel for the forward / dgrad layouts, the
+  // single-group asm-DMA schedule (var 4) for wgrad, where its 64-k steps measured faster
+  // (profiles/r01_gemm_variants*.log).  CLIPMI_GEMM_VAR overrides it for A/B runs.
+  static const int env_var = [] {
+    const char* e = getenv("CLIPMI_GEMM_VAR");
+    return e ? atoi(e) : -1;
+  }();
+  if (d->force_small_tile >= 2) p.var = d->force_small_tile;
+  else if (env_var >= 0 && d->force_small_tile == 0) p.var = env_var;
+  else p.var = (!d->a_kmajor && !d->b_kmajor) ? 4 : 0;
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
           ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
   // 256x256 LDS-DMA kernel for the big shapes (k-major operands need K % 64 == 0: the
