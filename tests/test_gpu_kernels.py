@@ -94,7 +94,9 @@ def attn_ref(qkv, B, N, H, mask, causal):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 50, 12, False), (2, 197, 12, False),
-                                           (3, 77, 8, True), (2, 256, 2, False)])
+                                           (3, 77, 8, True), (2, 256, 2, False),
+                                           # more (batch, head) items than the persistent grid
+                                           (90, 197, 12, False), (130, 77, 8, True)])
 def test_attention(dtype, B, N, H, causal):
     D = H * 64
     qkv = rnd((B * N, 3 * D), 11, dtype)

@@ -20,6 +20,8 @@
 // f32 path: exact-f32 SIMT kernels (4 lanes per row) for the fp32 parity mode.
 #include "common.h"
 #include "internal.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -156,6 +158,146 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p, int causal) {
       }
       if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? (mref + log2f(l)) * LN2 : NEG_INF;
     }
+  }
+}
+
+
+// ------------------------------------------------------------------- fwd, prefetching
+// Persistent variant of attn_fwd_mfma, which left the forward HBM-latency bound (one
+// (batch, head) per workgroup, K/V staged through VGPRs, nothing in flight while it
+// computes).  A workgroup of 8 waves walks (batch, head) items gridDim.x apart; the K and V
+// images of item i + 1 are LDS-DMA'd into the other half of a 2-slot ring, and each wave's
+// Q fragments for item i + 1 are loaded, while item i is computed.  DMAs are issued before
+// the Q loads so a wave's counted wait for its Q never waits on the ring.  Per wave: q-blocks
+// wave and wave + 8 of every item.
+template <int NKT, bool MASKED>
+__global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int nitems) {
+  constexpr int NPAD = NKT * 16, IMG = NPAD * 128, QPW = (NKT + 7) / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* keyok_base = (int*)(smem + 4 * IMG);  // [2][NPAD]
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int N = p.N, D = p.D, H = p.H;
+  const int64_t ld = 3 * (int64_t)D;
+  const int nqb = (N + 15) >> 4;
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const uint32_t rec = (uint32_t)((int64_t)(N - 1) * ld * 2 + 128);
+
+  auto issue = [&](int item, int slot) {  // K, V images of item into slot (rows >= N read 0)
+    const int b = item / H, h = item - b * H;
+    const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+    const SRsrc rk = make_srsrc(base + D, rec), rv = make_srsrc(base + 2 * D, rec);
+    char* kimg = smem + slot * 2 * IMG;
+    for (int j = wave; j < NPAD / 8; j += 8) {
+      const int r = 8 * j + (lane >> 3);
+      const int voff = r * (int)ld * 2 + (((lane & 7) ^ (r & 6)) << 4);
+      dma16(rk, kimg + j * 1024, voff);
+      dma16(rv, kimg + IMG + j * 1024, voff);
+    }
+    if (MASKED) {
+      int* ko = keyok_base + slot * NPAD;
+      for (int k = t; k < NPAD; k += 512) ko[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+    }
+  };
+  auto load_q = [&](int item, bf16x8 (&qf)[QPW][2]) {
+    const int b = item / H, h = item - b * H;
+    const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+      const int qc = min((wave + 8 * u) * 16 + li, N - 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) qf[u][kk] = *(const bf16x8*)(base + (int64_t)qc * ld + kk * 32 + 8 * g);
+    }
+  };
+
+  int item = blockIdx.x;
+  bf16x8 qn[QPW][2];
+  issue(item, 0);
+  load_q(item, qn);
+  for (int it = 0;; ++it) {
+    const int slot = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // slot ready for everyone; the other slot's last readers are done
+    const int cur = item, nxt = item + gridDim.x;
+    bf16x8 qf[QPW][2];
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) { qf[u][0] = qn[u][0]; qf[u][1] = qn[u][1]; }
+    if (nxt < nitems) {
+      issue(nxt, slot ^ 1);
+      load_q(nxt, qn);
+    }
+    const char* Kimg = smem + slot * 2 * IMG;
+    const char* Vimg = Kimg + IMG;
+    const int* keyok = keyok_base + slot * NPAD;
+    const int b = cur / H, h = cur - b * H;
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+      const int qb = wave + 8 * u;
+      if (qb >= nqb) break;
+      const int q = qb * 16 + li;
+      f32x4 s[NKT];
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[u][kk], s[kt], 0, 0, 0);
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (MASKED) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * 16 + 4 * g + r;
+            if (!(keyok[key] && (!causal || key <= q))) s[kt][r] = NEG_INF;
+          }
+        } else if (kt * 16 + 15 >= N) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kt * 16 + 4 * g + r >= N) s[kt][r] = NEG_INF;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mref = mx == NEG_INF ? 0.f : mx * c2;
+      float l = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c2, -mref));
+          s[kt][r] = e;
+          l += e;
+        }
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      f32x4 acc[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKT / 2; ++ks) {
+        const bf16x8 pf = pack8(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          acc[v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vimg, ks * 32, v * 16, lane), pf, acc[v], 0, 0, 0);
+      }
+      if (q < N) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        bf16* orow = p.o + ((int64_t)b * N + q) * D + h * 64;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float w[4] = {acc[v][0] * inv, acc[v][1] * inv, acc[v][2] * inv, acc[v][3] * inv};
+          store4(orow + v * 16 + 4 * g, w);
+        }
+        if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? (mref + __log2f(l)) * LN2 : NEG_INF;
+      }
+    }
+    item = nxt;
+    if (item >= nitems) break;
   }
 }
 
@@ -473,9 +615,38 @@ __global__ __launch_bounds__(1024) void attn_bwd_f32(AttnF p) {
   }
 }
 
+template <int NKT, bool M>
+void launch_fwd_pf(const AttnP& p, int causal, hipStream_t s) {
+  constexpr int NPAD = NKT * 16;
+  constexpr size_t lds = 4 * (size_t)NPAD * 128 + 2 * NPAD * sizeof(int);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_pf<NKT, M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nitems = p.B * p.H;
+  const int per_cu = (int)std::min<size_t>(2, (160 * 1024) / lds);
+  const int grid = std::min(nitems, 256 * per_cu);
+  hipLaunchKernelGGL((attn_fwd_pf<NKT, M>), dim3(grid), dim3(512), lds, s, p, causal, nitems);
+}
+
 template <bool M>
 int fwd_dispatch(const AttnP& p, int causal, hipStream_t s) {
   const int nkt = ((p.N + 31) & ~31) / 16;
+  static const bool old = [] { const char* e = getenv("CLIPMI_ATTN_FWD_OLD"); return e && atoi(e); }();
+  if (!old) {
+    switch (nkt) {
+      case 2: launch_fwd_pf<2, M>(p, causal, s); return CLIPMI_OK;
+      case 4: launch_fwd_pf<4, M>(p, causal, s); return CLIPMI_OK;
+      case 6: launch_fwd_pf<6, M>(p, causal, s); return CLIPMI_OK;
+      case 8: launch_fwd_pf<8, M>(p, causal, s); return CLIPMI_OK;
+      case 10: launch_fwd_pf<10, M>(p, causal, s); return CLIPMI_OK;
+      case 12: launch_fwd_pf<12, M>(p, causal, s); return CLIPMI_OK;
+      case 14: launch_fwd_pf<14, M>(p, causal, s); return CLIPMI_OK;
+      case 16: launch_fwd_pf<16, M>(p, causal, s); return CLIPMI_OK;
+      default: return clipmi_invalid("attention: N must be <= 256");
+    }
+  }
   const dim3 g(p.B * p.H), blk(256);
   switch (nkt) {
     case 2: hipLaunchKernelGGL((attn_fwd_mfma<2, M>), g, blk, 0, s, p, causal); break;

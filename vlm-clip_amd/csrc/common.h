@@ -65,3 +65,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 #define CLIPMI_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return clipmi_fail(e_, __FILE__, __LINE__); } while (0)
+// LDS-DMA (buffer_load_dwordx4 ... lds: 16 B per lane, 1 KiB per wave-instruction, written
+// lane-linearly at the wave-uniform LDS address) issued from inline asm.  hipcc's waitcnt pass treats every
+// ds_read_b64_tr_b16 as aliasing any LDS-DMA it can see and puts s_waitcnt vmcnt(0) in
+// front of it, which drains the next k-step's prefetch in the middle of the current one;
+// DMAs it cannot see are ordered by this kernel's own vmcnt + barrier instead.
+struct SRsrc { u32x4 v; };
+__device__ __forceinline__ SRsrc make_srsrc(const void* base, uint32_t num_records) {
+  const uint64_t b = (uint64_t)base;
+  SRsrc r;
+  r.v[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r.v[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xffffu);
+  r.v[2] = __builtin_amdgcn_readfirstlane(num_records);
+  r.v[3] = 0x00020000u;
+  return r;
+}
+__device__ __forceinline__ void dma16(SRsrc r, char* lds_wave_base, int voff) {
+  const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r.v)
+               : "memory");
+}
+
