@@ -175,14 +175,18 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    evs[0].record()
     for i in range(args.warmup, total):
         loss = step(i)
+        evs[i - args.warmup + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    log(f"timed {args.steps} steps: {elapsed:.3f} s")
+    log(f"timed {args.steps} steps: {elapsed:.3f} s; per-step GPU ms: "
+        + " ".join(f"{evs[k].elapsed_time(evs[k + 1]):.1f}" for k in range(args.steps)))
     L.clipmi_prof_disarm()
     ms = (ctypes.c_float * cap)()
     fl = (ctypes.c_double * cap)()

@@ -7,10 +7,12 @@
 // is written [B*N, D] so the out-projection GEMM consumes it directly.  The forward saves
 // the per-row log-sum-exp so the backward recomputes P without storing N x N scores.
 //
-// bf16 path (N <= 256): one workgroup per (batch, head).  K/V (and Q/dO in the backward)
-// live in LDS as [Npad][64] bf16 images with 16-B chunk c of row r stored at c ^ (r & 6);
-// that single swizzle is conflict-free for the ds_read_b128 fragment reads, the
-// ds_read_b64_tr_b16 transposed reads and the 16-B staging writes (tools/lds_banks.py).
+// bf16 path (N <= 256): persistent workgroups walk (batch, head) items; the next item's
+// operands are LDS-DMA'd while the current one is computed (attn_fwd_pf, attn_bwd_pf).
+// K/V (and Q/dO/O in the backward) live in LDS as [Npad][64] bf16 images with 16-B chunk
+// c of row r stored at c ^ (r & 6); that single swizzle is conflict-free for the
+// ds_read_b128 fragment reads, the ds_read_b64_tr_b16 transposed reads and the lane-linear
+// DMA writes (the swizzle is applied to the DMA source address).
 // Scores are computed "key-major" so each lane owns whole query rows: the row max/sum
 // need two xor-shuffles and the P tile feeds the next MFMA straight from registers
 // (cdna_hip_programming.md §3, accumulator as operand, with the k-permutation matched
@@ -69,103 +71,9 @@ struct AttnP {
   float scale;
 };
 
-// ----------------------------------------------------------------------------- fwd
-// MASKED = false: bidirectional, no key padding (vision) -> validity is key < N, tested only
-// in the boundary tile.  MASKED = true: key padding from LDS + optional causal (text).
-template <int NKT, bool MASKED>
-__global__ __launch_bounds__(256) void attn_fwd_mfma(AttnP p, int causal) {
-  constexpr int NPAD = NKT * 16;
-  __shared__ __attribute__((aligned(16))) char Kimg[NPAD * 128];
-  __shared__ __attribute__((aligned(16))) char Vimg[NPAD * 128];
-  __shared__ int keyok[MASKED ? NPAD : 1];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
-  const int N = p.N, D = p.D;
-  const int64_t ld = 3 * (int64_t)D;
-  const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
-  stage_img(Kimg, base + D, ld, N, NPAD, t, 256);
-  stage_img(Vimg, base + 2 * D, ld, N, NPAD, t, 256);
-  if (MASKED)
-    for (int k = t; k < NPAD; k += 256) keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
-  __syncthreads();
-
-  const float c2 = p.scale * LOG2E;
-  const int g = lane >> 4, li = lane & 15;
-  const int nqb = (N + 15) >> 4;
-  for (int qb = wave; qb < nqb; qb += 4) {
-    const int q = qb * 16 + li;
-    const int qc = min(q, N - 1);
-    bf16x8 qf[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) qf[kk] = *(const bf16x8*)(base + (int64_t)qc * ld + kk * 32 + 8 * g);
-    f32x4 s[NKT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
-    }
-    // s[kt][r] = raw score(q, key = kt*16 + 4g + r); invalid keys -> -inf
-    float mx = NEG_INF;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      if (MASKED) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kt * 16 + 4 * g + r;
-          if (!(keyok[key] && (!causal || key <= q))) s[kt][r] = NEG_INF;
-        }
-      } else if (kt * 16 + 15 >= N) {  // boundary tile only
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kt * 16 + 4 * g + r >= N) s[kt][r] = NEG_INF;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mref = mx == NEG_INF ? 0.f : mx * c2;
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(fmaf(s[kt][r], c2, -mref));
-        s[kt][r] = e;
-        l += e;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    f32x4 acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < NKT / 2; ++ks) {
-      const bf16x8 pf = pack8(s[2 * ks], s[2 * ks + 1]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vimg, ks * 32, u * 16, lane), pf, acc[u], 0, 0, 0);
-    }
-    if (q < N) {
-      const float inv = l > 0.f ? 1.f / l : 0.f;
-      bf16* orow = p.o + ((int64_t)b * N + q) * D + h * 64;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float v[4] = {acc[u][0] * inv, acc[u][1] * inv, acc[u][2] * inv, acc[u][3] * inv};
-        store4(orow + u * 16 + 4 * g, v);
-      }
-      if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? (mref + log2f(l)) * LN2 : NEG_INF;
-    }
-  }
-}
-
-
 // ------------------------------------------------------------------- fwd, prefetching
-// Persistent variant of attn_fwd_mfma, which left the forward HBM-latency bound (one
-// (batch, head) per workgroup, K/V staged through VGPRs, nothing in flight while it
-// computes).  A workgroup of 8 waves walks (batch, head) items gridDim.x apart; the K and V
+// Persistent forward.  (A first version ran one (batch, head) per workgroup with K/V
+// staged through VGPRs and nothing in flight while it computed: HBM-latency bound at 2.2 TB/s.)  A workgroup of 8 waves walks (batch, head) items gridDim.x apart; the K and V
 // images of item i + 1 are LDS-DMA'd into the other half of a 2-slot ring, and each wave's
 // Q fragments for item i + 1 are loaded, while item i is computed.  DMAs are issued before
 // the Q loads so a wave's counted wait for its Q never waits on the ring.  Per wave: q-blocks
@@ -189,6 +97,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
     const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
     const SRsrc rk = make_srsrc(base + D, rec), rv = make_srsrc(base + 2 * D, rec);
     char* kimg = smem + slot * 2 * IMG;
+#pragma unroll 1
     for (int j = wave; j < NPAD / 8; j += 8) {
       const int r = 8 * j + (lane >> 3);
       const int voff = r * (int)ld * 2 + (((lane & 7) ^ (r & 6)) << 4);
@@ -231,69 +140,87 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
     const char* Vimg = Kimg + IMG;
     const int* keyok = keyok_base + slot * NPAD;
     const int b = cur / H, h = cur - b * H;
+    {
+      // each of the wave's q-blocks (wave, wave + 8) computes its scores and softmax in turn and
+      // keeps P packed as bf16; the P.V products then run together, sharing every V read
+      int q[QPW];
+      float mref[QPW], l[QPW];
+      bf16x8 pf[QPW][NKT / 2];
 #pragma unroll
-    for (int u = 0; u < QPW; ++u) {
-      const int qb = wave + 8 * u;
-      if (qb >= nqb) break;
-      const int q = qb * 16 + li;
-      f32x4 s[NKT];
+      for (int u = 0; u < QPW; ++u) {
+        q[u] = (wave + 8 * u) * 16 + li;
+        f32x4 sc[NKT];
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < NKT; ++kt) {
+          sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[u][kk], s[kt], 0, 0, 0);
-      }
-      float mx = NEG_INF;
+          for (int kk = 0; kk < 2; ++kk)
+            sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, kt * 16 + li, kk * 4 + g), qf[u][kk], sc[kt], 0, 0, 0);
+        }
+        float mx = NEG_INF;
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-        if (MASKED) {
+        for (int kt = 0; kt < NKT; ++kt) {
+          if (MASKED) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = kt * 16 + 4 * g + r;
+              if (!(keyok[key] && (!causal || key <= q[u]))) sc[kt][r] = NEG_INF;
+            }
+          } else if (kt >= NKT - 2) {  // NPAD = N rounded up to 32: only the last two tiles hold padding
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (kt * 16 + 4 * g + r >= N) sc[kt][r] = NEG_INF;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mref[u] = mx == NEG_INF ? 0.f : mx * c2;
+        float lsum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int key = kt * 16 + 4 * g + r;
-            if (!(keyok[key] && (!causal || key <= q))) s[kt][r] = NEG_INF;
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], c2, -mref[u]));
+            sc[kt][r] = e;
+            lsum += e;
           }
-        } else if (kt * 16 + 15 >= N) {
+        lsum += __shfl_xor(lsum, 16, 64);
+        lsum += __shfl_xor(lsum, 32, 64);
+        l[u] = lsum;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (kt * 16 + 4 * g + r >= N) s[kt][r] = NEG_INF;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
+        for (int ks = 0; ks < NKT / 2; ++ks) pf[u][ks] = pack8(sc[2 * ks], sc[2 * ks + 1]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the blocks' score tiles from being live at once
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mref = mx == NEG_INF ? 0.f : mx * c2;
-      float l = 0.f;
+      f32x4 acc[QPW][4];
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+      for (int u = 0; u < QPW; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c2, -mref));
-          s[kt][r] = e;
-          l += e;
-        }
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-      f32x4 acc[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < 4; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKT / 2; ++ks) {
-        const bf16x8 pf = pack8(s[2 * ks], s[2 * ks + 1]);
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          acc[v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vimg, ks * 32, v * 16, lane), pf, acc[v], 0, 0, 0);
-      }
-      if (q < N) {
-        const float inv = l > 0.f ? 1.f / l : 0.f;
-        bf16* orow = p.o + ((int64_t)b * N + q) * D + h * 64;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float w[4] = {acc[v][0] * inv, acc[v][1] * inv, acc[v][2] * inv, acc[v][3] * inv};
-          store4(orow + v * 16 + 4 * g, w);
+          const bf16x8 tv = frag_tr(Vimg, ks * 32, v * 16, lane);
+#pragma unroll
+          for (int u = 0; u < QPW; ++u)
+            acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tv, pf[u][ks], acc[u][v], 0, 0, 0);
         }
-        if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? (mref + __log2f(l)) * LN2 : NEG_INF;
+      }
+#pragma unroll
+      for (int u = 0; u < QPW; ++u) {
+        if (wave + 8 * u < nqb && q[u] < N) {
+          const float inv = l[u] > 0.f ? 1.f / l[u] : 0.f;
+          bf16* orow = p.o + ((int64_t)b * N + q[u]) * D + h * 64;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            float w[4] = {acc[u][v][0] * inv, acc[u][v][1] * inv, acc[u][v][2] * inv, acc[u][v][3] * inv};
+            store4(orow + v * 16 + 4 * g, w);
+          }
+          if (g == 0)
+            p.lse[((int64_t)b * p.H + h) * N + q[u]] = l[u] > 0.f ? (mref[u] + __log2f(l[u])) * LN2 : NEG_INF;
+        }
       }
     }
     item = nxt;
@@ -469,6 +396,354 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_mfma(AttnP p) {  // 2 WGs per
   }
 }
 
+
+// ------------------------------------------------------------------- bwd, prefetching
+// Persistent backward: a workgroup of NW waves walks (batch, head) items gridDim.x apart.
+// Per item, LDS holds the Q, dO, O images (phase A + delta) and the K, V images (phase B):
+//   top:     wait for Q/dO/O(i) + meta(i); delta(i) = rowsum(dO * O) from the images
+//   phase A: DMA K/V(i) into their images while computing dK, dV (each wave owns 16 keys,
+//            K/V fragments in registers, loaded from global during phase B(i - 1))
+//   phase B: load item i + 1's K/V fragments and lse / key mask (plain loads, issued before
+//            any DMA so their waits never wait on the ring), copy this wave's Q/dO(i)
+//            fragments out of LDS, then DMA Q/dO/O(i + 1) over those images while computing
+//            dQ (each wave owns 16 queries, K/V images).
+// So every byte the next phase needs is in flight during the current one.  Barriers that
+// must not wait for those plain loads are raw s_barrier (lgkmcnt only).
+__device__ __forceinline__ void raw_barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+
+// Per-item context of the prefetching backward's two phases.
+struct BwdCtx {
+  const char *Qimg, *dOimg, *Kimg, *Vimg;
+  const float *lse2, *delta;
+  const int* keyok;
+  bf16* dq_base;  // dqkv + (b * N) * ld + h * 64
+  int64_t ld;
+  int N, NPAD, nstep, lane, D;
+  float c2, scale;
+};
+
+// dK, dV of the wave's NB key blocks (kb = wave, wave + NW): K/V fragments in registers,
+// Q/dO images in LDS.
+template <bool CAUSAL, int NB>
+__device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[2][2], const bf16x8 (&vf)[2][2],
+                                            int wave, int NW) {
+  const int lane = c.lane, g = lane >> 4, li = lane & 15;
+  bool kok[NB];
+  int key[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    key[u] = (wave + NW * u) * 16 + li;
+    kok[u] = c.keyok[key[u]];
+  }
+  f32x4 dv[NB][4], dk[NB][4];
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) { dv[u][v] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u][v] = dv[u][v]; }
+  for (int qs = 0; qs < c.nstep; ++qs) {
+    if (CAUSAL && qs * 32 + 31 < wave * 16) continue;  // every query of this step precedes every key
+    f32x4 pt[NB][2], ds[NB][2];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      const int qr = qs * 32 + tau * 16 + li;
+      bf16x8 qa[2], da[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        qa[kk] = frag_row(c.Qimg, qr, kk * 4 + g);
+        da[kk] = frag_row(c.dOimg, qr, kk * 4 + g);
+      }
+      const int q0 = qs * 32 + tau * 16 + 4 * g;
+      const f32x4 l4 = *LDS_PTR(const f32x4, c.lse2 + q0);
+      const f32x4 d4 = *LDS_PTR(const f32x4, c.delta + q0);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kf[u][kk], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[kk], vf[u][kk], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = kok[u] && (!CAUSAL || key[u] <= q0 + r);
+          const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l4[r]) : 0.f;
+          pt[u][tau][r] = pv;
+          ds[u][tau][r] = pv * (dp[r] - d4[r]);
+        }
+      }
+    }
+    bf16x8 pf[NB], sf[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      pf[u] = pack8(pt[u][0], pt[u][1]);
+      sf[u] = pack8(ds[u][0], ds[u][1]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const bf16x8 td = frag_tr(c.dOimg, qs * 32, v * 16, lane), tq = frag_tr(c.Qimg, qs * 32, v * 16, lane);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        dv[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(td, pf[u], dv[u][v], 0, 0, 0);
+        dk[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tq, sf[u], dk[u][v], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    if (key[u] < c.N) {
+      bf16* row = c.dq_base + (int64_t)key[u] * c.ld;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float a[4] = {dk[u][v][0] * c.scale, dk[u][v][1] * c.scale, dk[u][v][2] * c.scale, dk[u][v][3] * c.scale};
+        float w[4] = {dv[u][v][0], dv[u][v][1], dv[u][v][2], dv[u][v][3]};
+        store4(row + c.D + v * 16 + 4 * g, a);
+        store4(row + 2 * c.D + v * 16 + 4 * g, w);
+      }
+    }
+  }
+}
+
+// dQ of the wave's NB query blocks (qb = wave, wave + NW): Q/dO fragments in registers, K/V
+// images in LDS; the blocks advance together over the keys, sharing every K/V read.
+template <bool CAUSAL, int NB>
+__device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[2][2], const bf16x8 (&of)[2][2],
+                                            int wave, int NW) {
+  const int lane = c.lane, g = lane >> 4, li = lane & 15;
+  int q[NB];
+  float l2[NB], dl[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    q[u] = (wave + NW * u) * 16 + li;
+    l2[u] = c.lse2[q[u]];
+    dl[u] = c.delta[q[u]];
+  }
+  f32x4 dq[NB][4];
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dq[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kslim = CAUSAL ? min(c.nstep, ((wave + NW * (NB - 1)) * 16 + 15) / 32 + 1) : c.nstep;
+  for (int ks = 0; ks < kslim; ++ks) {
+    f32x4 ds[NB][2];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      const int kr = ks * 32 + tau * 16 + li;
+      bf16x8 ka[2], va[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ka[kk] = frag_row(c.Kimg, kr, kk * 4 + g);
+        va[kk] = frag_row(c.Vimg, kr, kk * 4 + g);
+      }
+      const int k0 = ks * 32 + tau * 16 + 4 * g;
+      const i32x4 ko = *LDS_PTR(const i32x4, c.keyok + k0);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[kk], qf[u][kk], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[kk], of[u][kk], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = ko[r] && (!CAUSAL || k0 + r <= q[u]);
+          const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l2[u]) : 0.f;
+          ds[u][tau][r] = pv * (dp[r] - dl[u]);
+        }
+      }
+    }
+    bf16x8 sf[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) sf[u] = pack8(ds[u][0], ds[u][1]);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const bf16x8 tk = frag_tr(c.Kimg, ks * 32, v * 16, lane);
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+        dq[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tk, sf[u], dq[u][v], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    if (q[u] < c.N) {
+      bf16* row = c.dq_base + (int64_t)q[u] * c.ld;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float a[4] = {dq[u][v][0] * c.scale, dq[u][v][1] * c.scale, dq[u][v][2] * c.scale, dq[u][v][3] * c.scale};
+        store4(row + v * 16 + 4 * g, a);
+      }
+    }
+  }
+}
+
+template <bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int N = p.N, D = p.D, H = p.H;
+  const int NPAD = (N + 31) & ~31, IMG = NPAD * 128;
+  const int64_t ld = 3 * (int64_t)D;
+  char* Qimg = smem;
+  char* dOimg = smem + IMG;
+  char* Oimg = smem + 2 * IMG;
+  char* Kimg = smem + 3 * IMG;
+  char* Vimg = smem + 4 * IMG;
+  float* arr = (float*)(smem + 5 * IMG);  // [2 slots][lse2 | delta | keyok][NPAD]
+  const uint32_t rec3 = (uint32_t)((int64_t)(N - 1) * ld * 2 + 128);
+  const uint32_t rec1 = (uint32_t)((int64_t)(N - 1) * D * 2 + 128);
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const int nkb = (N + 15) >> 4, nstep = NPAD >> 5;
+
+  auto qkv_of = [&](int item) {
+    const int b = item / H, h = item - b * H;
+    return p.qkv + (int64_t)b * N * ld + h * 64;
+  };
+  auto issue_qdo = [&](int item) {
+    const int b = item / H, h = item - b * H;
+    const SRsrc rq = make_srsrc(qkv_of(item), rec3);
+    const SRsrc rd = make_srsrc(p.dout + (int64_t)b * N * D + h * 64, rec1);
+    const SRsrc ro = make_srsrc(p.o + (int64_t)b * N * D + h * 64, rec1);
+#pragma unroll 1
+    for (int j = wave; j < NPAD / 8; j += NW) {
+      const int r = 8 * j + (lane >> 3), c = ((lane & 7) ^ (r & 6)) << 4;
+      dma16(rq, Qimg + j * 1024, r * (int)ld * 2 + c);
+      dma16(rd, dOimg + j * 1024, r * D * 2 + c);
+      dma16(ro, Oimg + j * 1024, r * D * 2 + c);
+    }
+  };
+  auto issue_kv = [&](int item) {
+    const bf16* base = qkv_of(item);
+    const SRsrc rk = make_srsrc(base + D, rec3), rv = make_srsrc(base + 2 * D, rec3);
+#pragma unroll 1
+    for (int j = wave; j < NPAD / 8; j += NW) {
+      const int r = 8 * j + (lane >> 3), c = ((lane & 7) ^ (r & 6)) << 4;
+      dma16(rk, Kimg + j * 1024, r * (int)ld * 2 + c);
+      dma16(rv, Vimg + j * 1024, r * (int)ld * 2 + c);
+    }
+  };
+  auto load_kvfrag = [&](int item, bf16x8 (&kf)[2][2], bf16x8 (&vf)[2][2]) {
+    const bf16* base = qkv_of(item);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int key = min((wave + NW * u) * 16 + li, N - 1);  // rows past N are masked by keyok
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        kf[u][kk] = *(const bf16x8*)(base + D + (int64_t)key * ld + kk * 32 + 8 * g);
+        vf[u][kk] = *(const bf16x8*)(base + 2 * D + (int64_t)key * ld + kk * 32 + 8 * g);
+      }
+    }
+  };
+  auto load_meta = [&](int item, float& l2v, int& kov) {
+    const int b = item / H, h = item - b * H;
+    l2v = __builtin_huge_valf();
+    kov = 0;
+    if (t < N) {
+      l2v = p.lse[((int64_t)b * H + h) * N + t] * LOG2E;
+      kov = !p.kmask || p.kmask[(int64_t)b * N + t] != 0;
+    }
+  };
+  auto store_meta = [&](int sl, float l2v, int kov) {
+    if (t < NPAD) {
+      arr[sl * 3 * NPAD + t] = l2v;
+      ((int*)arr)[sl * 3 * NPAD + 2 * NPAD + t] = kov;
+    }
+  };
+
+  int item = blockIdx.x;
+  bf16x8 kf[2][2], vf[2][2];
+  {
+    float l2v;
+    int kov;
+    load_kvfrag(item, kf, vf);
+    load_meta(item, l2v, kov);
+    issue_qdo(item);
+    store_meta(0, l2v, kov);
+  }
+  for (int it = 0;; ++it) {
+    const int sl = it & 1;
+    const float* lse2 = arr + sl * 3 * NPAD;
+    float* delta = arr + sl * 3 * NPAD + NPAD;
+    const int* keyok = (const int*)(arr + sl * 3 * NPAD + 2 * NPAD);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // Q/dO/O(i), meta(i) ready; K/V images free
+    const int cur = item, nxt = item + gridDim.x;
+    const int b = cur / H, h = cur - b * H;
+    const BwdCtx c{Qimg, dOimg, Kimg, Vimg, lse2, delta, keyok, p.dqkv + (int64_t)b * N * ld + h * 64, ld,
+                   N, NPAD, nstep, lane, D, c2, p.scale};
+    // delta[q] = sum_d dO * O, 8 lanes per row, from the LDS images
+    for (int id = t; id < NPAD * 8; id += NT) {
+      const int r = id >> 3, c = id & 7;
+      const bf16x8 a = frag_row(dOimg, r, c), o8 = frag_row(Oimg, r, c);
+      float sum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum = fmaf((float)a[e], (float)o8[e], sum);
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      if (c == 0) delta[r] = sum;
+    }
+    raw_barrier_lds();
+    issue_kv(cur);
+
+    // ---- phase A: dK, dV (Q image, dO image); a wave with two key blocks advances them
+    // together so each Q/dO fragment read from LDS feeds both
+    // (causal: blocks far apart need different query ranges, so they run one at a time)
+    if (!CAUSAL && wave + NW < nkb) {
+      bwd_phase_a<CAUSAL, 2>(c, kf, vf, wave, NW);
+    } else {
+      if (wave < nkb) bwd_phase_a<CAUSAL, 1>(c, kf, vf, wave, NW);
+      if (wave + NW < nkb) {
+        const bf16x8 kf1[2][2] = {{kf[1][0], kf[1][1]}, {kf[1][0], kf[1][1]}};
+        const bf16x8 vf1[2][2] = {{vf[1][0], vf[1][1]}, {vf[1][0], vf[1][1]}};
+        bwd_phase_a<CAUSAL, 1>(c, kf1, vf1, wave + NW, NW);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // K/V(i) images landed; phase A's reads of Q/dO done
+
+    // ---- phase B: dQ (K image, V image)
+    const bool more = nxt < nitems;
+    float l2n = 0.f;
+    int kon = 0;
+    if (more) {
+      load_kvfrag(nxt, kf, vf);
+      load_meta(nxt, l2n, kon);
+    }
+    const int nqb = (N + 15) >> 4;
+    bf16x8 qf[2][2], of[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = min((wave + NW * u) * 16, NPAD - 16) + li;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        qf[u][kk] = frag_row(Qimg, q, kk * 4 + g);
+        of[u][kk] = frag_row(dOimg, q, kk * 4 + g);
+      }
+    }
+    raw_barrier_lds();  // every wave holds its Q/dO fragments: the images may be overwritten
+    if (more) issue_qdo(nxt);
+    if (!CAUSAL && wave + NW < nqb) {
+      bwd_phase_b<CAUSAL, 2>(c, qf, of, wave, NW);
+    } else {
+      if (wave < nqb) bwd_phase_b<CAUSAL, 1>(c, qf, of, wave, NW);
+      if (wave + NW < nqb) {
+        const bf16x8 qf1[2][2] = {{qf[1][0], qf[1][1]}, {qf[1][0], qf[1][1]}};
+        const bf16x8 of1[2][2] = {{of[1][0], of[1][1]}, {of[1][0], of[1][1]}};
+        bwd_phase_b<CAUSAL, 1>(c, qf1, of1, wave + NW, NW);
+      }
+    }
+    if (!more) break;
+    store_meta(sl ^ 1, l2n, kon);  // slot sl ^ 1's readers (item i - 1) finished long ago
+    item = nxt;
+  }
+}
+
 // ------------------------------------------------------------------ f32 SIMT path
 // 4 lanes per row, 16 head dims each.  K/V (or Q/dO) staged in LDS as fp32 [N][64].
 struct AttnF {
@@ -633,35 +908,44 @@ void launch_fwd_pf(const AttnP& p, int causal, hipStream_t s) {
 template <bool M>
 int fwd_dispatch(const AttnP& p, int causal, hipStream_t s) {
   const int nkt = ((p.N + 31) & ~31) / 16;
-  static const bool old = [] { const char* e = getenv("CLIPMI_ATTN_FWD_OLD"); return e && atoi(e); }();
-  if (!old) {
-    switch (nkt) {
-      case 2: launch_fwd_pf<2, M>(p, causal, s); return CLIPMI_OK;
-      case 4: launch_fwd_pf<4, M>(p, causal, s); return CLIPMI_OK;
-      case 6: launch_fwd_pf<6, M>(p, causal, s); return CLIPMI_OK;
-      case 8: launch_fwd_pf<8, M>(p, causal, s); return CLIPMI_OK;
-      case 10: launch_fwd_pf<10, M>(p, causal, s); return CLIPMI_OK;
-      case 12: launch_fwd_pf<12, M>(p, causal, s); return CLIPMI_OK;
-      case 14: launch_fwd_pf<14, M>(p, causal, s); return CLIPMI_OK;
-      case 16: launch_fwd_pf<16, M>(p, causal, s); return CLIPMI_OK;
-      default: return clipmi_invalid("attention: N must be <= 256");
-    }
-  }
-  const dim3 g(p.B * p.H), blk(256);
   switch (nkt) {
-    case 2: hipLaunchKernelGGL((attn_fwd_mfma<2, M>), g, blk, 0, s, p, causal); break;
-    case 4: hipLaunchKernelGGL((attn_fwd_mfma<4, M>), g, blk, 0, s, p, causal); break;
-    case 6: hipLaunchKernelGGL((attn_fwd_mfma<6, M>), g, blk, 0, s, p, causal); break;
-    case 8: hipLaunchKernelGGL((attn_fwd_mfma<8, M>), g, blk, 0, s, p, causal); break;
-    case 10: hipLaunchKernelGGL((attn_fwd_mfma<10, M>), g, blk, 0, s, p, causal); break;
-    case 12: hipLaunchKernelGGL((attn_fwd_mfma<12, M>), g, blk, 0, s, p, causal); break;
-    case 14: hipLaunchKernelGGL((attn_fwd_mfma<14, M>), g, blk, 0, s, p, causal); break;
-    case 16: hipLaunchKernelGGL((attn_fwd_mfma<16, M>), g, blk, 0, s, p, causal); break;
+    case 2: launch_fwd_pf<2, M>(p, causal, s); return CLIPMI_OK;
+    case 4: launch_fwd_pf<4, M>(p, causal, s); return CLIPMI_OK;
+    case 6: launch_fwd_pf<6, M>(p, causal, s); return CLIPMI_OK;
+    case 8: launch_fwd_pf<8, M>(p, causal, s); return CLIPMI_OK;
+    case 10: launch_fwd_pf<10, M>(p, causal, s); return CLIPMI_OK;
+    case 12: launch_fwd_pf<12, M>(p, causal, s); return CLIPMI_OK;
+    case 14: launch_fwd_pf<14, M>(p, causal, s); return CLIPMI_OK;
+    case 16: launch_fwd_pf<16, M>(p, causal, s); return CLIPMI_OK;
     default: return clipmi_invalid("attention: N must be <= 256");
+  }
+}
+
+
+template <bool C, int NW>
+void launch_bwd_pf(const AttnP& p, hipStream_t s) {
+  const int npad = (p.N + 31) & ~31;
+  const size_t lds = 5 * (size_t)npad * 128 + 6 * (size_t)npad * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_pf<C, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int nitems = p.B * p.H;
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+  const int grid = std::min(nitems, 256 * per_cu);
+  hipLaunchKernelGGL((attn_bwd_pf<C, NW>), dim3(grid), dim3(NW * 64), lds, s, p, nitems);
+}
+// 4 waves per workgroup for N <= 128 (text: 5 blocks of 16 rows), else 8; each wave owns at
+// most 2 key blocks and 2 query blocks.
+int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
+  if (p.N <= 128) {
+    if (causal) launch_bwd_pf<true, 4>(p, s); else launch_bwd_pf<false, 4>(p, s);
+  } else {
+    if (causal) launch_bwd_pf<true, 8>(p, s); else launch_bwd_pf<false, 8>(p, s);
   }
   return CLIPMI_OK;
 }
-
 }  // namespace
 
 // attention_mask: int64 [B, N] key-padding mask (1 = keep) or NULL; causal: text tower.
@@ -712,8 +996,13 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
     }
     const double flops = 10.0 * B * H * (double)N * npad * 64;
     ProfScope ps(s, nullptr, flops);
-    if (causal) hipLaunchKernelGGL(attn_bwd_mfma<true>, dim3(B * H), dim3(512), lds, s, p);
-    else hipLaunchKernelGGL(attn_bwd_mfma<false>, dim3(B * H), dim3(512), lds, s, p);
+    if (5 * (size_t)npad * 128 + 6 * (size_t)npad * 4 <= 160 * 1024) {  // N <= 224: prefetching kernel
+      CLIPMI_TRY(bwd_pf_dispatch(p, causal, s));
+    } else if (causal) {
+      hipLaunchKernelGGL(attn_bwd_mfma<true>, dim3(B * H), dim3(512), lds, s, p);
+    } else {
+      hipLaunchKernelGGL(attn_bwd_mfma<false>, dim3(B * H), dim3(512), lds, s, p);
+    }
     ps.finish("attn_bwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D, causal, 0.125f};
