@@ -36,7 +36,7 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("akm,bkm", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("small", [0, 1, 4])  # production (ping-pong 256), 128 tile, single-group 256
+@pytest.mark.parametrize("small", [0, 1, 4, 11])  # production (ping-pong 256), 128 tile, single-group 256, half-tile pipeline
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 136, 72), (77, 64, 768), (1000, 512, 200),
                                    (1000, 776, 768), (600, 264, 1000), (512, 256, 64), (520, 384, 96),
                                    (768, 256, 4160)])

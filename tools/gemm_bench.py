@@ -1,10 +1,15 @@
-"""Per-shape GEMM throughput of libclipmi on the ViT-B/16 B=1024 training shapes (GPU)."""
+"""Per-shape GEMM throughput of libclipmi on the ViT-B/16 B=1024 training shapes (GPU).
+
+GEMM_VARIANTS=0,10 (force_small_tile values; 0 = production schedule) picks the schedules;
+every variant's output is checked against variant 0's on the same inputs (max rel diff);
+GEMM_TORCH=1 adds torch.matmul (hipBLASLt, plain product) for reference."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vlm-clip_amd"))
 import torch
 from clipmi import kernels as K, _lib
 
 R = 1024 * 197
+RT = 1024 * 77
 SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("fc1_fwd", R, 3072, 768, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("fc2_fwd", R, 768, 3072, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
@@ -13,23 +18,42 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("fc2_dgrad", R, 3072, 768, True, False, torch.bfloat16, _lib.EPI_DQGELU, 1),
     ("fc1_dgrad", R, 768, 3072, True, False, torch.bfloat16, 0, 1),
     ("qkv_dgrad", R, 768, 2304, True, False, torch.bfloat16, 0, 1),
+    ("out_dgrad", R, 768, 768, True, False, torch.bfloat16, 0, 1),
     ("fc1_wgrad", 3072, 768, R, False, False, torch.float32, _lib.EPI_BETA, 2),
     ("fc2_wgrad", 768, 3072, R, False, False, torch.float32, _lib.EPI_BETA, 2),
     ("qkv_wgrad", 2304, 768, R, False, False, torch.float32, _lib.EPI_BETA, 2),
-    ("out_wgrad", 768, 768, R, False, False, torch.float32, _lib.EPI_BETA, 8),
+    ("out_wgrad", 768, 768, R, False, False, torch.float32, _lib.EPI_BETA, 2),
+    ("t_fc1_fwd", RT, 2048, 512, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
+    ("t_fc2_fwd", RT, 512, 2048, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    ("t_qkv_fwd", RT, 1536, 512, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
     # reference points (not on the CLIP path): square, operands resident in MALL
     ("sq4k", 4096, 4096, 4096, True, True, torch.bfloat16, 0, 1),
     ("sq8k", 8192, 8192, 8192, True, True, torch.bfloat16, 0, 1),
-    ("fc2_fwd_l2", 16384, 768, 3072, True, True, torch.bfloat16, 0, 1),
 ]
-VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,1").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,10").split(",")]
+REPS = int(os.environ.get("GEMM_REPS", "10"))
 only = sys.argv[1:] if len(sys.argv) > 1 else None
+
+
+def timeit(f, n=REPS):
+    for _ in range(2):
+        f()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(n):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
 torch.manual_seed(0)
 for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
-    if (only and name not in only) or (not only and name in ("sq4k", "sq8k", "fc2_fwd_l2")):
+    if (only and name not in only) or (not only and name in ("sq4k", "sq8k")):
         continue
-    A = torch.randn(M * Kd, device="cuda").to(torch.bfloat16)
-    B = torch.randn(N * Kd, device="cuda").to(torch.bfloat16)
+    A = (torch.rand(M * Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N * Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
     lda = Kd if akm else M
     ldb = Kd if bkm else N
     C = torch.zeros(M, N, device="cuda", dtype=odt)
@@ -39,6 +63,8 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     if split == 2:  # engine's choice for 256 tiles
         tiles = ((M + 255) // 256) * ((N + 255) // 256)
         split = max(1, min(32, 512 // tiles))
+        while split > 1 and Kd // split < 512:
+            split -= 1
     ws = torch.empty(split * M * N, device="cuda") if split > 1 else None
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,
@@ -46,34 +72,24 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     if os.environ.get("GEMM_TORCH"):  # hipBLASLt via torch.matmul, plain product, for comparison
         a2 = A.view(M, Kd) if akm else A.view(Kd, M).t()
         b2 = B.view(N, Kd).t() if bkm else B.view(Kd, N)
-        g = lambda: torch.matmul(a2, b2)
-        for _ in range(3):
-            g()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ms = timeit(lambda: torch.matmul(a2, b2))
+        print(f"{name:10s} torch M={M} N={N} K={Kd}: {ms * 1e3:8.1f} us {2 * M * N * Kd / ms / 1e9:7.1f} TF/s",
+              flush=True)
+    ref = None
+    for v in VARIANTS:  # 0 = production schedule, 1 = 128 tile, >= 2: 256-kernel schedule
+        kw2 = dict(kw, bias_grad=None) if (v == 1 and bg is not None) else kw
+        f = lambda: K.gemm(M, N, Kd, A, lda, akm, B, ldb, bkm, C, N, small_tile=v, **kw2)
+        C.zero_()
+        f()
         torch.cuda.synchronize()
-        e0.record()
-        for _ in range(10):
-            g()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 10
-        print(f"{name:10s} torch M={M} N={N} K={Kd}: {ms * 1e3:8.1f} us {2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
-    for small in VARIANTS:  # 0 = production schedule, 1 = 128 tile, 2 = up-front DMA issue
-        if small == 1 and bg is not None:
-            kw2 = dict(kw, bias_grad=None)
+        out = C.float().clone()
+        if ref is None:
+            ref, err = out, 0.0
         else:
-            kw2 = kw
-        f = lambda: K.gemm(M, N, Kd, A, lda, akm, B, ldb, bkm, C, N, small_tile=small, **kw2)
-        for _ in range(3):
-            f()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record()
-        n = 10
-        for _ in range(n):
-            f()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / n
-        print(f"{name:10s} v{small} M={M} N={N} K={Kd} split={split}: {ms * 1e3:8.1f} us "
-              f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
+            err = ((out - ref).abs().max() / ref.abs().max().clamp_min(1e-6)).item()
+        del out
+        ms = timeit(f)
+        print(f"{name:10s} v{v} M={M} N={N} K={Kd} split={split}: {ms * 1e3:8.1f} us "
+              f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s  maxrel-vs-v{VARIANTS[0]} {err:.2e}", flush=True)
+    del A, B, C, aux, res, ws, ref
+    torch.cuda.empty_cache()

@@ -24,9 +24,12 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
-__device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// sigmoid(1.702 x) through v_exp + v_rcp (1 ulp) instead of an IEEE division sequence:
+// these run per output element in the GEMM epilogues
+__device__ __forceinline__ float qg_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x)); }
+__device__ __forceinline__ float quick_gelu(float x) { return x * qg_sigmoid(x); }
 __device__ __forceinline__ float quick_gelu_grad(float x) {
-  float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  const float s = qg_sigmoid(x);
   return s + 1.702f * x * s * (1.0f - s);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }

@@ -55,15 +55,45 @@ int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool 
   return clipmi_gemm(s, &d);
 }
 
-// split-K factor for a wgrad GEMM [M x N] reducing over K tokens
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    n = c;
+  }
+  return n;
+}
+
+// split-K factor for a wgrad GEMM [M x N] reducing over K tokens.  bf16 (256x256 tiles, one
+// workgroup per CU): the smallest split whose workgroups fill whole rounds of the chip best,
+// with >= 512 tokens per slab.  ViT-B/16 out-proj (768x768 = 9 tiles): 28 splits = 252
+// workgroups in one round, where a fixed 512-workgroup target gave 32 = 288, a second round
+// 1/8 full; text out-proj (4 tiles): 64 splits instead of 32 that left half the chip idle.
 int wgrad_splits(int M, int N, int K, int dt) {
   const int tile = dt == CLIPMI_BF16 ? 256 : 64;
-  const int target = dt == CLIPMI_BF16 ? 512 : 1024;  // workgroups: 2 waves of the 256-CU chip
   const int tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
-  int s = std::max(1, target / std::max(1, tiles));
-  s = std::min(s, 32);
-  while (s > 1 && (int64_t)K / s < 512) --s;
-  return s;
+  if (dt != CLIPMI_BF16) {
+    int s = std::max(1, 1024 / std::max(1, tiles));
+    s = std::min(s, 32);
+    while (s > 1 && (int64_t)K / s < 512) --s;
+    return s;
+  }
+  const int cus = cu_count();
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= 64; ++s) {
+    if (s > 1 && (int64_t)K / s < 512) break;
+    const int64_t wg = (int64_t)tiles * s;
+    const int64_t rounds = (wg + cus - 1) / cus;
+    const double eff = (double)wg / (double)(rounds * cus);
+    if (eff > best_eff + 0.02) {
+      best = s;
+      best_eff = eff;
+    }
+  }
+  return best;
 }
 
 struct WsPlan {

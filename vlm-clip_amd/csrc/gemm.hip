@@ -45,6 +45,7 @@ struct GemmP {
   int tiles_n, ntiles;
   int vec;  // all leading dimensions multiples of 4 elements
   int var;  // 256-kernel main-loop schedule (0 production)
+  int vec8; // bf16 C with N, ldc/ldr/ldaux multiples of 8 and C/res/aux/bias 16-B aligned
 };
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
@@ -428,13 +429,107 @@ __device__ __forceinline__ void epilogue256(const GemmP& p, f32x4 (&acc)[8][4], 
   }
 }
 
+// 8 consecutive bf16 as float (one 16-B access)
+__device__ __forceinline__ void load8(const bf16* p, float v[8]) {
+  const bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = (float)t[r];
+}
+__device__ __forceinline__ void store8(bf16* p, const float v[8]) {
+  *(bf16x8*)p = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+}
+
+// bf16-output epilogue with 16-B accesses (cdna_hip_programming.md T21, 16-lane form).  The
+// 16x16 accumulator layout gives a lane 4 consecutive columns per fragment, i.e. 8-B stores of
+// 16 rows x 32 B per instruction, and those epilogues were store-issue bound.  One
+// v_permlane16_swap per accumulator dword pairs fragments (2jp, 2jp+1): afterwards lane
+// row-group q = lane>>4 holds 8 consecutive columns, fragment 2jp + (q & 1), columns
+// 8*(q >> 1) .. +7, so every residual/aux load and every store is one 16-B access covering
+// 16 rows x 64 B per instruction: half the memory instructions for the same bytes.
+template <int EPI>
+__device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
+  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
+  constexpr bool HAUX = HDQ || HDG;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);  // this lane's column within a fragment pair
+  float bv[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const int n = min(nb + 32 * jp + coff, p.N - 8);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) {
+        load4((const float*)p.bias + n, bv[jp]);
+        load4((const float*)p.bias + n + 4, bv[jp] + 4);
+      } else {
+        load8((const bf16*)p.bias + n, bv[jp]);
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float xin[4][2][8];
+    if (HR || HAUX || HBETA) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int n = min(nb + 32 * jp + coff, p.N - 8);
+          if (HR) load8((const bf16*)p.res + (int64_t)m * p.ldr + n, xin[ii][jp]);
+          else if (HAUX) load8((const bf16*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][jp]);
+          else load8((const bf16*)p.C + (int64_t)m * p.ldc + n, xin[ii][jp]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = h * 4 + ii;
+      const int m = mb + i * 16 + mlane;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int n = nb + 32 * jp + coff;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // swapped right before use: no extra live registers
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
+          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+        }
+        const bool ok = m < p.M && n < p.N;
+        if (HPRE && ok) store8((bf16*)p.aux + (int64_t)m * p.ldaux + n, v);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (HQ) v[r] = quick_gelu(v[r]);
+          if (HG) v[r] = gelu_erf(v[r]);
+          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][jp][r]);
+          if (HDG) v[r] *= gelu_erf_grad(xin[ii][jp][r]);
+          if (HR || HBETA) v[r] += xin[ii][jp][r];
+        }
+        if (ok) store8((bf16*)p.C + (int64_t)m * p.ldc + n, v);
+      }
+    }
+  }
+}
+
 // Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
-// allows it (4-aligned columns, aligned leading dims), else the per-subtile generic path
-// (split-K slabs, ragged N, runtime flags).
+// allows it (4-aligned columns, aligned leading dims; the 16-B form for bf16 output when
+// columns, leading dims and pointers allow 16-B accesses), else the per-subtile generic path
+// (split-K slab kz, ragged N, runtime flags).
 template <typename OutT, int EPI>
-__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane, int kz) {
   constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
                         !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
+  if constexpr (FAST && std::is_same<OutT, bf16>::value) {
+    if (!p.ws && p.vec8) {
+      epilogue256_w<EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
+      return;
+    }
+  }
   if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
     epilogue256<OutT, EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
     return;
@@ -448,7 +543,7 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
       const int n = nb + j * 16 + (lane >> 4) * 4;
       if (n >= p.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.ws) st4(p.ws + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
+      if (p.ws) st4(p.ws + (int64_t)kz * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
       else epilogue4<OutT, EPI>(p, m, n, v);
     }
   }
@@ -460,10 +555,13 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int tile = xcd_remap(blockIdx.x, p.ntiles);
+  // 1-D grid over (split, tile), XCD-aware over all of it: an XCD walks a contiguous run of
+  // tiles of one k-slab, so that slab's A and B panels are fetched into its L2 once
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kz = wid / p.ntiles, tile = wid - kz * p.ntiles;
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BT, n0 = tn * BT;
-  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kbeg = kz * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
   const bf16* A = (const bf16*)p.A;
@@ -554,7 +652,7 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
       if (m < p.M) atomicAdd(bias_grad + m, accb[i][0]);
     }
   }
-  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz);
 }
 
 // ------------------------------------------------------------------ ping-pong 256x256 path
@@ -647,10 +745,13 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int tile = xcd_remap(blockIdx.x, p.ntiles);
+  // 1-D grid over (split, tile), XCD-aware over all of it: an XCD walks a contiguous run of
+  // tiles of one k-slab, so that slab's A and B panels are fetched into its L2 once
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kz = wid / p.ntiles, tile = wid - kz * p.ntiles;
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BT, n0 = tn * BT;
-  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kbeg = kz * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int ns = (kend - kbeg + 31) / 32;
   const bf16* A = (const bf16*)p.A;
@@ -728,7 +829,260 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
       if (m < p.M) atomicAdd(bias_grad + m, accb[mh][0]);
     }
   }
-  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz);
+}
+
+// ------------------------------------------------------------------ persistent ping-pong
+// gemm_pp_kernel's schedule over a flattened stream of (tile, k-stage) pairs.  A workgroup
+// walks its tiles gridDim.x apart and the LDS ring runs straight across tile boundaries, so
+// the first PP_D stages of the next tile are DMA'd while the current tile's last stages and
+// its epilogue run: no pipeline fill per tile, and one wave group's epilogue (VALU + stores)
+// runs beside the other group's MFMA section.  Tiles are visited in groups of PP_GM
+// row-blocks (every column-block of a group before the next group), so the 32 tiles an
+// XCD holds at once share a few row and column panels in its L2.
+constexpr int PP_GM = 8;
+
+__device__ __forceinline__ void pps_tile(const GemmP& p, int lin, int& m0, int& n0) {
+  const int tiles_m = p.ntiles / p.tiles_n;
+  const int grp = lin / (PP_GM * p.tiles_n);
+  const int rem = lin - grp * PP_GM * p.tiles_n;
+  const int rows = min(PP_GM, tiles_m - grp * PP_GM);
+  const int tn = rem / rows;
+  const int tm = grp * PP_GM + (rem - tn * rows);
+  m0 = tm * BT;
+  n0 = tn * BT;
+}
+
+template <bool AK, bool BKM, typename OutT, int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm_pps_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x;
+  const int r = xcd_remap(blockIdx.x, G);     // same-XCD workgroups take consecutive slots of a round
+  const int nt = (p.ntiles - r + G - 1) / G;  // this workgroup's tiles: rounds j with j*G + r < ntiles
+  const int ns = (p.K + 31) / 32;             // k-stages per tile
+  const int S = nt * ns;
+  const bf16* A = (const bf16*)p.A;
+  const bf16* B = (const bf16*)p.B;
+
+  // issue stream position: tile ij, stage ik, that tile's origin
+  int ij = 0, ik = 0, im0, in0;
+  pps_tile(p, r, im0, in0);
+  auto advance_issue = [&]() {
+    if (++ik == ns) {
+      ik = 0;
+      ++ij;
+      if (ij < nt) pps_tile(p, ij * G + r, im0, in0);
+    }
+  };
+  auto slot = [&](int gs) { return smem + (gs % PP_S) * PP_STAGE; };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < PP_D; ++st) {  // prologue: stages 0 .. PP_D - 1 of the stream
+    if (st < S) {
+      stage_pp<AK>(slot(st), A, p.lda, im0, p.M, ik * 32, p.K, wave, lane);
+      stage_pp<BKM>(slot(st) + 16384, B, p.ldb, in0, p.N, ik * 32, p.K, wave, lane);
+      advance_issue();
+    }
+  }
+  pp_vmcnt(4 * (min(PP_D, S) - 1));  // stage 0 landed
+  pp_barrier();
+  if (wm == 1) pp_barrier();
+
+  int cj = 0, ck = 0, cm0, cn0;  // consumed tile, its stage, its origin
+  pps_tile(p, r, cm0, cn0);
+  for (int gs = 0; gs < S; ++gs) {
+    const char* img = slot(gs);
+    char* nimg = slot(gs + PP_D);
+    const bool issue = gs + PP_D < S;
+    bf16x8 fb[4];
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      bf16x8 fa[4];
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = read_frag_pp<BKM>(img + 16384, wn * 64 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag_pp<AK>(img, wm * 128 + (ph * 4 + i) * 16, lane);
+      if (issue) {
+        if (ph == 0) {
+          stage_pp<AK>(nimg, A, p.lda, im0, p.M, ik * 32, p.K, wave, lane);
+        } else {
+          stage_pp<BKM>(nimg + 16384, B, p.ldb, in0, p.N, ik * 32, p.K, wave, lane);
+          advance_issue();
+        }
+      }
+      if (ph == 1) pp_vmcnt(4 * max(0, min(PP_D - 1, S - gs - 2)));  // stage gs + 1 landed
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ph * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[ph * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+    if (++ck == ns) {  // tile done: its epilogue runs while the next tile's first stages land
+      finish256<OutT, EPI>(p, acc, cm0 + wm * 128, cn0 + wn * 64, lane, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ck = 0;
+      if (++cj < nt) pps_tile(p, cj * G + r, cm0, cn0);
+    }
+  }
+  if (wm == 0) pp_barrier();  // pairs with group 1's leading barrier
+}
+
+// ------------------------------------------------------------------ half-tile pipeline, BK = 64
+// gemm_pp_kernel's ping-pong schedule with every LDS-DMA piece made of full 128-B lines.  With
+// BK = 32 stages a k-major piece is 16 rows x 64 B, twice the texture-address requests per
+// byte of an 8-row x 128-B piece (cdna_hip_programming.md §5, "Projection GEMM at M = 256":
+// 16 x 64 B pieces ran TA_BUSY 2x at equal traffic).  Here K advances in K-tiles of 64 through
+// two 64 KiB buffers (A image [256][128 B] | B image, gemm256_kernel's layouts), and a K-tile
+// arrives as four 16 KiB half-tiles (2 pieces per wave each) in the order they are first read:
+//   i = 0: A m-half 0 (rows 0..63 and 128..191: the first 64 rows of each wave group)
+//   i = 1, 2: B rows (k-major) or columns (k-row image) 0..127 / 128..255
+//   i = 3: A m-half 1 (rows 64..127 and 192..255)
+// A K-tile is consumed in 4 phases of 16 MFMAs per wave, one per quadrant of the wave's 128x64
+// block: (m-half 0, n-half 0) reads the A m-half 0 and B n-half 0 fragments, (0, 1) B n-half 1,
+// (1, 0) A m-half 1, (1, 1) nothing.  Half-tile s = 4t + i is issued in phase s - HP_D and
+// waited for (counted vmcnt(6) / vmcnt(8)) in every wave's load section of the phase before its
+// first read, i.e. before the barrier ahead of that read (the staggered group reads one
+// interval later).  It overwrites half-tile s - 8, whose last fragment reads (phase s - 8 or
+// s - 9 + i) both groups retired (lgkmcnt, in their MFMA section) at least one interval before
+// the overwrite is issued.
+constexpr int HP_D = 6;
+
+template <bool BKM>
+__device__ __forceinline__ void stage_hp(char* buf, const SRsrc& ra, int64_t lda, const SRsrc& rb, int64_t ldb, int i,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = wave * 2 + u;  // piece 0..15 of the half-tile, 1 KiB each
+    if (i == 0 || i == 3) {      // A rows g*128 + mh*64 + 8*(j & 7) .. +7, g = j >> 3
+      const int r = (j >> 3) * 128 + (i == 3 ? 64 : 0) + (j & 7) * 8;
+      const int rr = r + (lane >> 3);
+      const int c = (lane & 7) ^ ((rr >> 1) & 7);
+      dma16(ra, buf + r * 128, (int)((int64_t)rr * lda * 2 + c * 16));
+    } else if (BKM) {            // B k-major: rows 128*(i-1) + 8j .. +7
+      const int r = (i - 1) * 128 + j * 8;
+      const int rr = r + (lane >> 3);
+      const int c = (lane & 7) ^ ((rr >> 1) & 7);
+      dma16(rb, buf + 32768 + r * 128, (int)((int64_t)rr * ldb * 2 + c * 16));
+    } else {                     // B k-row: half image i-1, k rows 4j .. 4j+3
+      const int h = i - 1;
+      const int kr = 4 * j + (lane >> 4);
+      const int c = (lane & 15) ^ mimg_swz(kr);
+      dma16(rb, buf + 32768 + h * 16384 + j * 1024, (int)((int64_t)kr * ldb * 2 + (h * 128 + c * 8) * 2));
+    }
+  }
+}
+
+// the 16 MFMAs of quadrant (MH, NH): A m-half MH fragments x B n-half NH fragments, k = 64
+template <int MH, int NH>
+__device__ __forceinline__ void hp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[4][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[MH * 4 + i][NH * 2 + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[NH * 2 + j][kk], fa[i][kk], acc[MH * 4 + i][NH * 2 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <bool BKM, typename OutT, int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm_hp_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int nk = (p.K + 63) >> 6, S = 4 * nk;
+  const bf16* A = (const bf16*)p.A;
+  const bf16* B = (const bf16*)p.B;
+  auto issue = [&](int s) {  // this wave's pieces of half-tile s of the stream
+    const int kt = s >> 2;
+    const SRsrc ra = srsrc256<true>(A, p.lda, m0, p.M, kt * 64, p.K);
+    const SRsrc rb = srsrc256<BKM>(B, p.ldb, n0, p.N, kt * 64, p.K);
+    stage_hp<BKM>(smem + (kt & 1) * 65536, ra, p.lda, rb, p.ldb, s & 3, wave, lane);
+  };
+  // half-tiles 0 .. issued-1 are issued: wait until half-tile `need` has landed
+  auto wait_for = [&](int issued, int need) { pp_vmcnt(2 * min(4, max(0, issued - 1 - need))); };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = 0; s < HP_D && s < S; ++s) issue(s);
+  wait_for(min(HP_D, S), min(2, S - 1));  // K-tile 0: A m-half 0 and both B halves
+  pp_barrier();
+  if (wm == 1) pp_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* ia = smem + (kt & 1) * 65536;
+    const char* ib = ia + 32768;
+    const int s0 = 4 * kt + HP_D;  // half-tile issued in this K-tile's phase 0
+    bf16x8 fa[4][2], fb[4][2];
+    // ---- phase 0: quadrant (0, 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = read_frag256<true>(ia, wm * 128 + i * 16, kk, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = read_frag256<BKM>(ib, wn * 64 + j * 16, kk, lane);
+    if (s0 < S) issue(s0);
+    pp_barrier();
+    hp_mfma<0, 0>(acc, fa, fb);
+    pp_barrier();
+    // ---- phase 1: quadrant (0, 1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[2 + j][kk] = read_frag256<BKM>(ib, wn * 64 + 32 + j * 16, kk, lane);
+    if (s0 + 1 < S) issue(s0 + 1);
+    wait_for(min(s0 + 2, S), 4 * kt + 3);  // this K-tile's A m-half 1, read in phase 2
+    pp_barrier();
+    hp_mfma<0, 1>(acc, fa, fb);
+    pp_barrier();
+    // ---- phase 2: quadrant (1, 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = read_frag256<true>(ia, wm * 128 + 64 + i * 16, kk, lane);
+    if (s0 + 2 < S) issue(s0 + 2);
+    pp_barrier();
+    hp_mfma<1, 0>(acc, fa, fb);
+    pp_barrier();
+    // ---- phase 3: quadrant (1, 1)
+    if (s0 + 3 < S) issue(s0 + 3);
+    if (kt + 1 < nk) wait_for(min(s0 + 4, S), 4 * kt + 6);  // next K-tile's A m-half 0 + B halves
+    pp_barrier();
+    hp_mfma<1, 1>(acc, fa, fb);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();  // pairs with group 1's leading barrier
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, 0);
 }
 
 // ------------------------------------------------------------------ f32 SIMT path
@@ -813,7 +1167,7 @@ void launch256v(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>), dim3(p.ntiles, splits), dim3(NT2), 131072, s,
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>), dim3(p.ntiles * splits), dim3(NT2), 131072, s,
                      p, bias_grad);
 }
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG, int PPV>
@@ -824,13 +1178,57 @@ void launch_ppv(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_S * PP_STAGE);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>), dim3(p.ntiles, splits), dim3(NT2),
+  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>), dim3(p.ntiles * splits), dim3(NT2),
                      PP_S * PP_STAGE, s, p, bias_grad);
+}
+int num_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  dev &= 63;
+  if (!n[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    n[dev] = c;
+  }
+  return n[dev];
+}
+template <bool AK, bool BKM, typename OutT, int EPI>
+void launch_pps(const GemmP& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_pps_kernel<AK, BKM, OutT, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_S * PP_STAGE);
+    attr = true;
+  }
+  const int grid = std::min(p.ntiles, num_cus());  // one 160 KiB workgroup per CU
+  hipLaunchKernelGGL((gemm_pps_kernel<AK, BKM, OutT, EPI>), dim3(grid), dim3(NT2), PP_S * PP_STAGE, s, p);
+}
+template <bool BKM, typename OutT, int EPI>
+void launch_hp(const GemmP& p, hipStream_t s) {
+  static bool attr = false;  // two 64 KiB K-tile buffers
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_hp_kernel<BKM, OutT, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              131072);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_hp_kernel<BKM, OutT, EPI>), dim3(p.ntiles), dim3(NT2), 131072, s, p);
 }
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
 void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  // var 0 / 9: the ping-pong kernel; 4: gemm256_kernel VAR 3 (interleaved asm DMAs, the wgrad
-  // production schedule); 2 -> VAR 0 (all DMAs up front), 3 -> VAR 2 (builtin DMAs) for A/B.
+  // var 0 / 9: the ping-pong kernel; 10: its persistent form; 4: gemm256_kernel VAR 3
+  // (interleaved asm DMAs, the wgrad production schedule); 2 -> VAR 0 (all DMAs up front),
+  // 3 -> VAR 2 (builtin DMAs) for A/B.
+  if (p.var == 10 && !BG && !p.ws && splits == 1) {
+    launch_pps<AK, BKM, OutT, EPI>(p, s);
+    return;
+  }
+  if constexpr (AK && !BG) {  // var 11: half-tile pipeline (k-major A)
+    if (p.var == 11 && !p.ws && splits == 1) {
+      launch_hp<BKM, OutT, EPI>(p, s);
+      return;
+    }
+  }
   switch (p.var) {
     case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
     case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
@@ -959,15 +1357,25 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   // 256-kernel schedule: the ping-pong kernel for the forward / dgrad layouts, the
   // single-group asm-DMA schedule (var 4) for wgrad, where its 64-k steps measured faster
   // (profiles/r01_gemm_variants*.log).  CLIPMI_GEMM_VAR overrides it for A/B runs.
+  // (CLIPMI_GEMM_VAR: forward/dgrad layouts, CLIPMI_GEMM_WVAR: wgrad layout)
   static const int env_var = [] {
     const char* e = getenv("CLIPMI_GEMM_VAR");
     return e ? atoi(e) : -1;
   }();
+  static const int env_wvar = [] {
+    const char* e = getenv("CLIPMI_GEMM_WVAR");
+    return e ? atoi(e) : -1;
+  }();
+  const bool wlayout = !d->a_kmajor && !d->b_kmajor;
+  const int evar = wlayout ? env_wvar : env_var;
   if (d->force_small_tile >= 2) p.var = d->force_small_tile;
-  else if (env_var >= 0 && d->force_small_tile == 0) p.var = env_var;
-  else p.var = (!d->a_kmajor && !d->b_kmajor) ? 4 : 0;
+  else if (evar >= 0 && d->force_small_tile == 0) p.var = evar;
+  else p.var = wlayout ? 4 : 0;
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
           ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
+  p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&
+           ((uintptr_t)d->C % 16 == 0) && ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0) &&
+           ((uintptr_t)d->bias % 16 == 0);
   // 256x256 LDS-DMA kernel for the big shapes (k-major operands need K % 64 == 0: the
   // buffer range check zero-fills rows, not a row's k tail)
   const bool kok = (!d->a_kmajor || d->K % 64 == 0) && (!d->b_kmajor || d->K % 64 == 0);
