@@ -76,6 +76,20 @@ def synthetic_batch(cfg, B, rank, device, seed=1234):
     return {"input_ids": ids, "attention_mask": mask, "pixel_values": px.contiguous()}
 
 
+def wgrad_algorithmic_bytes(cfg, B):
+    """Mean compulsory HBM bytes of one gemm256_wgrad_splitk launch in a step: both bf16
+    operands read once (tokens x (M + N) x 2 B) + the fp32 gradient written once (M x N x 4 B),
+    over the step's 97 wgrad launches (4 per encoder layer per tower + the patch embedding)."""
+    v, t = cfg.vision_config, cfg.text_config
+    shapes = []
+    for tc, R in ((v, B * ((v.image_size // v.patch_size) ** 2 + 1)), (t, B * t.max_position_embeddings)):
+        D, F = tc.hidden_size, tc.intermediate_size
+        shapes += [(R, D, F), (R, F, D), (R, D, D), (R, 3 * D, D)] * tc.num_hidden_layers
+    shapes.append((B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, 3 * v.patch_size ** 2))
+    tot = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes)
+    return round(tot / len(shapes))
+
+
 def cpu_baseline(cfg, B, steps):
     """Oracle (oracle/clip_ref.py) full fine-tune step on the host: fwd + bwd + AdamW."""
     from clipmi import synth
@@ -200,6 +214,19 @@ def main():
     fwd = C.forward_flops_per_pair(cfg)
     step_flops_pair = 3 * fwd if not adapters else fwd
     roof = None
+    traffic, traffic_src = None, None
+    # HBM bytes per launch of the same kernel family from the committed PMC passes
+    # (tools/traffic_pmc.sh -> profiles/*_traffic.json; newest file wins)
+    import glob
+    tfiles = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    for tf in reversed(tfiles):
+        try:
+            tj = json.load(open(tf))
+        except (OSError, ValueError):
+            continue
+        if tj.get("kernel") == args.roofline_kernel:
+            traffic, traffic_src = tj["bytes_per_launch"], os.path.relpath(tf, REPO)
+            break
     if n > 0:
         avg_ms = sum(ms[i] for i in range(n)) / n
         avg_fl = sum(fl[i] for i in range(n)) / n
@@ -207,7 +234,9 @@ def main():
         roof = {"bound": "mfma", "kernel": args.roofline_kernel, "launches": n,
                 "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": avg_fl,
                 "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None}
+                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                "algorithmic_bytes": wgrad_algorithmic_bytes(cfg, args.batch)}
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),

@@ -26,6 +26,10 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("t_fc1_fwd", RT, 2048, 512, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("t_fc2_fwd", RT, 512, 2048, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
     ("t_qkv_fwd", RT, 1536, 512, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
+    # the same shapes with K = 64: prologue + epilogue cost per tile
+    ("fc1_k64", R, 3072, 64, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
+    ("qkv_k64", R, 2304, 64, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
+    ("fc2d_k64", R, 3072, 64, True, False, torch.bfloat16, _lib.EPI_DQGELU, 1),
     # reference points (not on the CLIP path): square, operands resident in MALL
     ("sq4k", 4096, 4096, 4096, True, True, torch.bfloat16, 0, 1),
     ("sq8k", 8192, 8192, 8192, True, True, torch.bfloat16, 0, 1),
@@ -50,7 +54,7 @@ def timeit(f, n=REPS):
 
 torch.manual_seed(0)
 for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
-    if (only and name not in only) or (not only and name in ("sq4k", "sq8k")):
+    if (only and name not in only) or (not only and (name in ("sq4k", "sq8k") or name.endswith("_k64"))):
         continue
     A = (torch.rand(M * Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
     B = (torch.rand(N * Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -60,11 +64,16 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     bias = torch.randn(N, device="cuda").to(torch.bfloat16)
     aux = torch.randn(M, N, device="cuda").to(odt) if flags & (_lib.EPI_DQGELU | _lib.EPI_STORE_PRE) else None
     res = torch.randn(M, N, device="cuda").to(odt) if flags & _lib.EPI_RESID else None
-    if split == 2:  # engine's choice for 256 tiles
+    if split == 2:  # engine.cpp wgrad_splits: the smallest split filling whole rounds of 256 CUs best
         tiles = ((M + 255) // 256) * ((N + 255) // 256)
-        split = max(1, min(32, 512 // tiles))
-        while split > 1 and Kd // split < 512:
-            split -= 1
+        split, best = 1, 0.0
+        for sp in range(1, 65):
+            if sp > 1 and Kd // sp < 512:
+                break
+            wg = tiles * sp
+            eff = wg / (256 * ((wg + 255) // 256))
+            if eff > best + 0.02:
+                split, best = sp, eff
     ws = torch.empty(split * M * N, device="cuda") if split > 1 else None
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,

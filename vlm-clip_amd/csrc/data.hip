@@ -29,6 +29,33 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* px, T* X, int 
   }
 }
 
+// Vectorised form for P % 8 == 0 (ViT-B/16, B/32): one thread per 8 consecutive k of a token
+// row, i.e. 8 consecutive kx of one pixel row: two 16-B loads, one 16-B (bf16) store; a wave
+// stores 1 KiB contiguous.  The scalar kernel above remains for other patch sizes (L/14).
+template <typename T>
+__global__ __launch_bounds__(256) void im2col8_kernel(const float* px, T* X, int64_t rows, int C, int Hh, int P, int G,
+                                                      int K, int Kp) {
+  const int gpr = Kp >> 3;
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = id / gpr;
+  if (row >= rows) return;
+  const int k = (int)(id - row * gpr) * 8;
+  const int Np1 = G * G + 1;
+  const int b = (int)(row / Np1), t = (int)(row - (int64_t)b * Np1);
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (t > 0 && k < K) {
+    const int p = t - 1, gy = p / G, gx = p - gy * G;
+    const int c = k / (P * P), r = k - c * P * P, ky = r / P, kx = r - ky * P;
+    const float* src = px + (((int64_t)b * C + c) * Hh + gy * P + ky) * Hh + gx * P + kx;
+    const f32x4 a = *(const f32x4*)src, a2 = *(const f32x4*)(src + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = a2[j]; }
+  }
+  T* dst = X + row * Kp + k;
+  store4(dst, v);
+  store4(dst + 4, v + 4);
+}
+
 // idx[b] = pooled token: mode 0 -> 0, mode 1 -> first position with id == eos, mode 2 -> argmax id
 __global__ void pool_index_kernel(const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -74,6 +101,14 @@ extern "C" int clipmi_im2col(void* stream, int dtype, const float* pixels, void*
   CLIPMI_REQUIRE(Kp >= K && Kp % 8 == 0, "Kp must be >= C*P*P and a multiple of 8");
   const int64_t rows = (int64_t)B * (G * G + 1);
   if (rows == 0) return CLIPMI_OK;
+  if (P % 8 == 0 && H % 4 == 0 && ((uintptr_t)pixels & 15) == 0 && ((uintptr_t)X & 15) == 0) {
+    const int64_t n = rows * (Kp / 8);
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(im2col8_kernel<bf16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (bf16*)X, rows, C, H, P, G, K, Kp);
+    else hipLaunchKernelGGL(im2col8_kernel<float>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (float*)X, rows, C, H, P, G, K, Kp);
+    CLIPMI_CHECK_LAUNCH();
+    return CLIPMI_OK;
+  }
   dim3 g((Kp + 255) / 256 > 4 ? 4 : (Kp + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535),
          (unsigned)((rows + 65534) / 65535));
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(im2col_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, pixels, (bf16*)X, B, C, H, P, G, K, Kp);

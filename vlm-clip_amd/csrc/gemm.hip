@@ -46,6 +46,7 @@ struct GemmP {
   int vec;  // all leading dimensions multiples of 4 elements
   int var;  // 256-kernel main-loop schedule (0 production)
   int vec8; // bf16 C with N, ldc/ldr/ldaux multiples of 8 and C/res/aux/bias 16-B aligned
+  int stagger, first_round;  // s_sleep(127) count for half of the first round's workgroups
 };
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
@@ -768,6 +769,12 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
   const bf16x8 ones = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
 
   auto slot = [&](int st) { return smem + (st % PP_S) * PP_STAGE; };
+  // first-round stagger: half the workgroups of every XCD start later, and since each CU
+  // takes its next workgroup when the previous one ends, the offset persists: one half's
+  // epilogue stores run beside the other half's main loop instead of all CUs storing at once
+  if (p.stagger > 0 && (int)blockIdx.x < p.first_round && ((blockIdx.x >> 3) & 1)) {
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   // prologue: stages 0 .. PP_D - 1
 #pragma unroll
   for (int st = 0; st < PP_D; ++st) {
@@ -829,6 +836,13 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
       if (m < p.M) atomicAdd(bias_grad + m, accb[mh][0]);
     }
   }
+  if constexpr (PPV & 8) {  // timing experiment: main loop only, results kept live, nothing stored
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
+    return;
+  }
   finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz);
 }
 
@@ -868,6 +882,9 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pps_kernel(GemmP p) {
   const bf16* B = (const bf16*)p.B;
 
   // issue stream position: tile ij, stage ik, that tile's origin
+  if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {  // half of every XCD's workgroups start later
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   int ij = 0, ik = 0, im0, in0;
   pps_tile(p, r, im0, in0);
   auto advance_issue = [&]() {
@@ -1234,6 +1251,7 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
     case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
     case 4: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
     case 9: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
+    case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); break;  // no epilogue (timing)
 #ifdef CLIPMI_GEMM_EXPERIMENTS
     case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
     case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
@@ -1368,7 +1386,12 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }();
   const bool wlayout = !d->a_kmajor && !d->b_kmajor;
   const int evar = wlayout ? env_wvar : env_var;
-  if (d->force_small_tile >= 2) p.var = d->force_small_tile;
+  p.stagger = 0;
+  p.first_round = num_cus();
+  if (d->force_small_tile >= 100) {  // A/B hook: 1xx ping-pong, 2xx persistent, with a stagger of xx
+    p.var = d->force_small_tile >= 200 ? 10 : 0;
+    p.stagger = d->force_small_tile % 100;
+  } else if (d->force_small_tile >= 2) p.var = d->force_small_tile;
   else if (evar >= 0 && d->force_small_tile == 0) p.var = evar;
   else p.var = wlayout ? 4 : 0;
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&

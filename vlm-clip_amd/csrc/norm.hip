@@ -213,27 +213,48 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* x, int64_t
 }
 
 // periodic row sums: out[t][c] (+)= sum_b x[(b*period + t)*ldx + c]   (position-embedding grads)
+// out[t][c..c+3] (+)= sum_b x[b*period + t][c..c+3] (position / class embedding gradients).
+// One block per (column chunk of 256, position t); its 4 waves split the batch (rows b = w,
+// w + 4, ...) with 8 independent loads in flight per lane, then add their partial sums in a
+// fixed order through LDS (deterministic).  The one-thread-per-column form it replaces kept one
+// load in flight per lane: latency bound at ~1 TB/s.
 template <typename T>
 __global__ __launch_bounds__(256) void period_sum_kernel(const T* x, int64_t ldx, int nb, int period, int D,
                                                          float* out, int beta) {
-  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  __shared__ f32x4 part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
   const int t = blockIdx.y;
-  if (c >= D) return;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b = 0; b < nb; ++b) {
-    float v[4];
-    load4(x + ((int64_t)b * period + t) * ldx + c, v);
+  if (c < D) {
+    int b = w;
+    for (; b + 28 < nb; b += 32) {
+      float v[8][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] += v[j];
-  }
-  float* o = out + (int64_t)t * D + c;
-  if (beta) {
-    float ov[4];
-    load4(o, ov);
+      for (int u = 0; u < 8; ++u) load4(x + ((int64_t)(b + 4 * u) * period + t) * ldx + c, v[u]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] += ov[j];
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += v[u][j];
+    }
+    for (; b < nb; b += 4) {
+      float v[4];
+      load4(x + ((int64_t)b * period + t) * ldx + c, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += v[j];
+    }
   }
-  store4(o, s);
+  part[w][lane] = f32x4{s[0], s[1], s[2], s[3]};
+  __syncthreads();
+  if (w == 0 && c < D) {
+    f32x4 a = part[0][lane];
+    a += part[1][lane];
+    a += part[2][lane];
+    a += part[3][lane];
+    float* o = out + (int64_t)t * D + c;
+    if (beta) a += *(const f32x4*)o;
+    *(f32x4*)o = a;
+  }
 }
 
 // x0[r] = tok[ids[r]] + pos[r % S]
@@ -457,7 +478,7 @@ extern "C" int clipmi_period_sum(void* stream, int dtype, const void* x, int64_t
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D % 4 == 0, "D % 4");
   CLIPMI_REQUIRE(nt >= 1 && nt <= period, "nt must be in [1, period]");
-  dim3 g((D / 4 + 255) / 256, nt);
+  dim3 g((D / 4 + 63) / 64, nt);
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(period_sum_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, nb, period, D, out, beta);
   else hipLaunchKernelGGL(period_sum_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, nb, period, D, out, beta);
   CLIPMI_CHECK_LAUNCH();
