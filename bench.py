@@ -175,9 +175,12 @@ def main():
         return loss
 
     for i in range(args.warmup):
+        t_w = time.perf_counter()
         step(i)
         torch.cuda.synchronize()
-        log(f"warmup step {i} done")
+        ms_ = torch.cuda.memory_stats(dev)
+        log(f"warmup step {i} done in {time.perf_counter() - t_w:.3f} s (allocator retries "
+            f"{ms_.get('num_alloc_retries')}, device mallocs {ms_.get('num_device_alloc')})")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -201,6 +204,10 @@ def main():
     elapsed = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {elapsed:.3f} s; per-step GPU ms: "
         + " ".join(f"{evs[k].elapsed_time(evs[k + 1]):.1f}" for k in range(args.steps)))
+    ms_ = torch.cuda.memory_stats(dev)
+    log(f"allocator: retries {ms_.get('num_alloc_retries')} device-mallocs {ms_.get('num_device_alloc')} "
+        f"frees {ms_.get('num_device_free')} reserved peak {ms_.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB "
+        f"allocated peak {ms_.get('allocated_bytes.all.peak', 0) / 2**30:.1f} GiB")
     L.clipmi_prof_disarm()
     ms = (ctypes.c_float * cap)()
     fl = (ctypes.c_double * cap)()

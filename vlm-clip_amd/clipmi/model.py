@@ -43,6 +43,29 @@ def _anchor(module: nn.Module):
     return next(module.parameters())
 
 
+class _JoinOnBackward(torch.autograd.Function):
+    """Identity on the text tower's output.  Its backward runs on the side stream (autograd runs a
+    node on its forward's stream) ahead of the rest of the text tower's backward, and queues a
+    final callback that makes the stream backward() was called on wait for the side stream, so
+    the optimizer sees the text tower's gradients (written straight into the grad arena)."""
+
+    @staticmethod
+    def forward(ctx, x, main, side):
+        ctx.side = side
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side = ctx.side
+        dev = side.device
+
+        def join():
+            torch.cuda.current_stream(dev).wait_stream(side)
+
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+        return g, None, None
+
+
 class CLIPWithAdapters(nn.Module):
     """CLIP model with text and vision adapters (model_m.py:10-248)."""
 
@@ -192,13 +215,40 @@ class CLIPWithAdapters(nn.Module):
         return T.PoolProjFn.apply(h, self.clip.visual_projection.weight, self._rt, "visual_projection.weight", None)
 
     # ------------------------------------------------------------------ forward
+    def _overlap_ok(self, input_ids, attention_mask, pixel_values):
+        """Run the text tower on a second HIP stream beside the vision tower (forward and, through
+        autograd's per-node streams, backward): the two towers' kernels fill each other's tail
+        rounds.  Safe when the towers share no gradient state that backward initialises on one
+        stream: the clip arena's grads are attached by ContrastiveFn (on the caller's stream)
+        before either tower's backward when logit_scale trains, and adapters have one arena each."""
+        if os.environ.get("CLIPMI_OVERLAP", "1") == "0" or input_ids is None or attention_mask is None:
+            return False
+        if pixel_values is None or not isinstance(pixel_values, torch.Tensor) or not pixel_values.is_cuda:
+            return False
+        if self.clip.arena.device.type != "cuda":
+            return False
+        if not torch.is_grad_enabled() or not self.clip.arena.any_requires_grad():
+            return True
+        return self.clip.logit_scale.requires_grad
+
+    def _side_stream(self):
+        dev = self.clip.arena.device
+        st = getattr(self, "_side", None)
+        if st is None or st.device != dev:
+            st = torch.cuda.Stream(device=dev)
+            self._side = st
+        return st
+
     def forward(self, input_ids=None, attention_mask=None, pixel_values=None, return_loss=True):
         """model_m.py:127-176."""
-        if input_ids is not None and attention_mask is not None:
-            text_features = self.get_text_features(input_ids, attention_mask)
+        if self._overlap_ok(input_ids, attention_mask, pixel_values):
+            text_features, image_features = self._both_towers_overlapped(input_ids, attention_mask, pixel_values)
         else:
-            text_features = None
-        image_features = self.get_image_features(pixel_values) if pixel_values is not None else None
+            if input_ids is not None and attention_mask is not None:
+                text_features = self.get_text_features(input_ids, attention_mask)
+            else:
+                text_features = None
+            image_features = self.get_image_features(pixel_values) if pixel_values is not None else None
         if return_loss and text_features is not None and image_features is not None:
             group = self.process_group
             loss, t, i, lpt, lpi = T.ContrastiveFn.apply(text_features, image_features, self.clip.logit_scale,
@@ -207,6 +257,22 @@ class CLIPWithAdapters(nn.Module):
             return {"loss": loss, "text_features": t, "image_features": i, "logits_per_text": lpt,
                     "logits_per_image": lpt.t() if world == 1 else lpi}
         return {"text_features": text_features, "image_features": image_features}
+
+    def _both_towers_overlapped(self, input_ids, attention_mask, pixel_values):
+        main = torch.cuda.current_stream(self.clip.arena.device)
+        side = self._side_stream()
+        for a in self.arenas():  # bf16 shadows refreshed on the caller's stream, before the fork
+            a.sync_shadow()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for t in (input_ids, attention_mask):
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(side)
+            text_features = _JoinOnBackward.apply(self.get_text_features(input_ids, attention_mask), main, side)
+        image_features = self.get_image_features(pixel_values)
+        main.wait_stream(side)
+        text_features.record_stream(main)
+        return text_features, image_features
 
     # ------------------------------------------------------------------ checkpoints
     def save_adapter_weights(self, save_path):

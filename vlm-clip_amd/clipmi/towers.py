@@ -266,6 +266,10 @@ class VisionTowerFn(torch.autograd.Function):
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
              arena.ptr("vision_model.embeddings.position_embedding.weight", g), 1)
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, 1, D, arena.ptr("vision_model.embeddings.class_embedding", g), 1)
+        # activations are released with backward, not with the graph object (a caller holding
+        # last step's loss would otherwise keep them alive into the next forward: 2x memory and
+        # fresh device mallocs mid-step); stream-ordered reuse keeps the queued kernels safe
+        ctx.buf = ctx.acts = ctx.X = ctx.h0 = ctx.stats0 = None
         return None, None, None
 
 
@@ -335,6 +339,7 @@ class TextTowerFn(torch.autograd.Function):
              arena.ptr("text_model.embeddings.token_embedding.weight", g), 1, P_(ews), ews.numel())
         call("clipmi_period_sum", s, dc, P_(dx), D, B, S, S, D,
              arena.ptr("text_model.embeddings.position_embedding.weight", g), 1)
+        ctx.buf = ctx.acts = ctx.xL = ctx.stats = None  # released with backward (see VisionTowerFn)
         return None, None, None, None
 
 
@@ -418,6 +423,7 @@ class AdapterFn(torch.autograd.Function):
         dx = torch.empty(R, Dh, dtype=dtype, device=dev)
         K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
                flags=_lib.EPI_RESID)
+        ctx.save = None  # released with backward (see VisionTowerFn)
         return dx.view(ctx.shape), None, None, None, None
 
 
@@ -468,6 +474,7 @@ class PoolProjFn(torch.autograd.Function):
         K.gemm(B, D, E, d, E, True, W, D, False, dpooled, D)
         dh = torch.zeros(B, S, D, dtype=dtype, device=dev)
         call("clipmi_scatter_rows", s, dc, P_(dpooled), P_(idx), B, S, D, P_(dh), 0)
+        ctx.save = None
         return dh, None, None, None, None
 
 
