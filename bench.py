@@ -189,6 +189,10 @@ def main():
     L.clipmi_prof_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
     cap = 4096
     _lib.check(L.clipmi_prof_arm(args.roofline_kernel.encode(), cap), "prof_arm")
+    # only the caller's stream: the text tower's launches run on a second stream beside the
+    # vision tower's kernels (model.py), so their event spans include the other tower's work
+    L.clipmi_prof_stream.argtypes = [ctypes.c_void_p]
+    _lib.check(L.clipmi_prof_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "prof_stream")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

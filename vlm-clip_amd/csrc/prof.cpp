@@ -11,12 +11,14 @@ struct Prof {
   std::vector<double> flops;
   int used = 0;
   int cap = 0;
+  hipStream_t only = nullptr;  // launches on other streams are not recorded
 } g;
 }  // namespace
 
 ProfScope::ProfScope(hipStream_t stream, const char* label, double flops) : s(stream), slot(-1) {
   if (!g.armed || g.used >= g.cap) return;
   if (label && g.variant != label) return;
+  if (g.only && stream != g.only) return;
   slot = g.used;
   (void)hipEventRecord(g.ev[2 * slot], s);
 }
@@ -45,6 +47,11 @@ extern "C" int clipmi_prof_arm(const char* variant, int max_launches) {
   g.used = 0;
   g.variant = variant;
   g.armed = true;
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_prof_stream(void* stream) {
+  g.only = (hipStream_t)stream;
   return CLIPMI_OK;
 }
 
