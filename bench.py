@@ -77,12 +77,13 @@ def synthetic_batch(cfg, B, rank, device, seed=1234):
 
 
 def wgrad_algorithmic_bytes(cfg, B):
-    """Mean compulsory HBM bytes of one gemm256_wgrad_splitk launch in a step: both bf16
-    operands read once (tokens x (M + N) x 2 B) + the fp32 gradient written once (M x N x 4 B),
-    over the step's 97 wgrad launches (4 per encoder layer per tower + the patch embedding)."""
-    v, t = cfg.vision_config, cfg.text_config
+    """Mean compulsory HBM bytes of one gemm256_wgrad_splitk launch the live roofline times:
+    both bf16 operands read once (tokens x (M + N) x 2 B) + the fp32 gradient written once
+    (M x N x 4 B), over the vision tower's 49 wgrad launches per step (4 per encoder layer +
+    the patch embedding; the text tower's run on the second stream and are not timed)."""
+    v = cfg.vision_config
     shapes = []
-    for tc, R in ((v, B * ((v.image_size // v.patch_size) ** 2 + 1)), (t, B * t.max_position_embeddings)):
+    for tc, R in ((v, B * ((v.image_size // v.patch_size) ** 2 + 1)),):
         D, F = tc.hidden_size, tc.intermediate_size
         shapes += [(R, D, F), (R, F, D), (R, D, D), (R, 3 * D, D)] * tc.num_hidden_layers
     shapes.append((B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, 3 * v.patch_size ** 2))

@@ -175,7 +175,8 @@ int clipmi_cast_f32_bf16(void* stream, const float* src, void* dst, int64_t n);
  * fills per-launch milliseconds and algorithmic FLOPs. */
 int clipmi_prof_arm(const char* variant, int max_launches);
 int clipmi_prof_disarm(void);
-/* Restrict the armed profiler to launches on one HIP stream (NULL = any): with the towers on
+/* Restrict the armed profiler to launches on one HIP stream (which may be the null stream):
+ * with the towers on
  * two streams, launches on the side stream share the GPU with the other tower's kernels and
  * their event-bracketed durations are not the kernel's own. */
 int clipmi_prof_stream(void* stream);

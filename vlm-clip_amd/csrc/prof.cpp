@@ -11,14 +11,15 @@ struct Prof {
   std::vector<double> flops;
   int used = 0;
   int cap = 0;
-  hipStream_t only = nullptr;  // launches on other streams are not recorded
+  bool filter = false;        // record only launches on `only` (which may be the null stream)
+  hipStream_t only = nullptr;
 } g;
 }  // namespace
 
 ProfScope::ProfScope(hipStream_t stream, const char* label, double flops) : s(stream), slot(-1) {
   if (!g.armed || g.used >= g.cap) return;
   if (label && g.variant != label) return;
-  if (g.only && stream != g.only) return;
+  if (g.filter && stream != g.only) return;
   slot = g.used;
   (void)hipEventRecord(g.ev[2 * slot], s);
 }
@@ -52,6 +53,7 @@ extern "C" int clipmi_prof_arm(const char* variant, int max_launches) {
 
 extern "C" int clipmi_prof_stream(void* stream) {
   g.only = (hipStream_t)stream;
+  g.filter = true;
   return CLIPMI_OK;
 }
 
