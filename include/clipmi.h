@@ -100,6 +100,12 @@ int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids, const voi
 /* vision: Conv2d(k=s=P, no bias) as im2col + GEMM ([HF] :148-154, :211-212).  X is
  * [B*(G*G+1), Kp] with a zero row in each image's CLS slot, K index c*P*P+ky*P+kx. */
 int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, int C, int H, int P, int Kp);
+/* The input step (CLIPImageProcessor's center_crop + rescale + normalize, [HF]
+ * image_processing_clip.py) fused into the same im2col: uint8 images [B, Hin, Win, 3]
+ * (channels last), centre-cropped to image_size, (u/255 - mean[c]) / std[c].  Resizing
+ * stays on the host.  P % 8 == 0, Kp == 3*P*P; mean/std are 3 host floats. */
+int clipmi_im2col_u8(void* stream, int dtype, const uint8_t* images, void* X, int B, int Hin, int Win, int image_size,
+                     int P, int Kp, const float* mean, const float* std);
 /* pooled token per row: mode 0 first token (model_m.py:102), 1 first EOS, 2 argmax id ([HF] :561-581) */
 int clipmi_pool_index(void* stream, const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx);
 int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* out);

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -94,6 +95,19 @@ def text_tower(input_ids, attention_mask, p, cfg):
     for i in range(t.num_hidden_layers):
         x = encoder_layer(x, p, f"{pre}.encoder.layers.{i}", t.num_attention_heads, t.layer_norm_eps, mask)
     return layer_norm(x, p[f"{pre}.final_layer_norm.weight"], p[f"{pre}.final_layer_norm.bias"], t.layer_norm_eps)
+
+
+def image_processor(images, image_size, mean, std):
+    """The input step of the reference (CLIPProcessor.from_pretrained(...) -> CLIPImageProcessor,
+    model_m.py:30, dataset.py:152-164) without resize: [HF] image_processing_clip.py
+    center_crop (top = (h - crop) // 2, left = (w - crop) // 2), rescale (x / 255), normalize
+    ((x - mean) / std), channels first.  uint8 [B, H, W, 3] numpy -> float32 [B, 3, S, S]."""
+    B, H, W, C = images.shape
+    top, left = (H - image_size) // 2, (W - image_size) // 2
+    x = images[:, top:top + image_size, left:left + image_size, :].astype(np.float32)
+    x = x * np.float32(1.0 / 255.0)
+    x = (x - np.asarray(mean, dtype=np.float32)) / np.asarray(std, dtype=np.float32)
+    return np.ascontiguousarray(x.transpose(0, 3, 1, 2)).astype(np.float32)
 
 
 def patch_embed(pixel_values, p, cfg):

@@ -245,3 +245,23 @@ def test_adamw_and_clip_match_torch():
         assert abs(norm[0].item() - tn.item()) < 1e-3 * tn.item()
     assert rel(p, p_ref.detach()) < 1e-5
     assert rel(shadow, p_ref.detach()) < 1e-2
+
+
+@pytest.mark.parametrize("tag", ["sq", "crop"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_im2col_uint8_matches_processor(golden, tag, dtype):
+    """Fused input step (uint8 NHWC -> crop + rescale + normalise + im2col) vs im2col of the
+    reference processor's pixel_values (tests/golden/image_processor.npz)."""
+    g = golden("image_processor.npz")
+    imgs = torch.from_numpy(g[f"{tag}_images"]).cuda()
+    pv = torch.from_numpy(g[f"{tag}_pixel_values"]).cuda()
+    B, P, S = imgs.shape[0], 16, 224
+    Kp = 3 * P * P
+    R = B * ((S // P) ** 2 + 1)
+    X = torch.full((R, Kp), 7.0, device="cuda", dtype=dtype)
+    T.im2col_uint8(imgs, X, S, P)
+    Xr = torch.empty(R, Kp, device="cuda", dtype=dtype)
+    T.call("clipmi_im2col", kern.stream(), DT[dtype], pv.data_ptr(), Xr.data_ptr(), B, 3, S, P, Kp)
+    torch.cuda.synchronize()
+    tol = 2e-6 if dtype == torch.float32 else 2e-2
+    assert (X.float() - Xr.float()).abs().max().item() < tol

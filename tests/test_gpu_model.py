@@ -124,3 +124,24 @@ def test_training_reduces_loss_bf16():
     tr = CLIPAdapterTrainer(m, [b], learning_rate=1e-3, output_dir="/tmp/clipmi_ck", trainable="requires_grad")
     losses = [tr.train_step(b, i, 20).item() for i in range(20)]
     assert losses[-1] < losses[0] * 0.8, losses
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_uint8_images_match_processor_path(precision):
+    """uint8 channels-last images through the fused input step give the logits of the
+    reference's path (CLIPImageProcessor pixel_values; oracle.image_processor, pinned by
+    tests/golden/image_processor.npz) on the same model and captions."""
+    from oracle import clip_ref as R
+    from clipmi import towers as T
+    m = make("tiny", False, precision, freeze=True)
+    cfg = m.config
+    rng = np.random.default_rng(5)
+    imgs = rng.integers(0, 256, (2, 72, 80, 3), dtype=np.uint8)
+    pv = R.image_processor(imgs, cfg.vision_config.image_size, T.IMAGE_MEAN, T.IMAGE_STD)
+    b = batch(cfg, 2)
+    with torch.no_grad():
+        a = m(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=torch.from_numpy(pv).cuda())
+        u = m(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=torch.from_numpy(imgs).cuda())
+    torch.cuda.synchronize()
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    assert (a["logits_per_text"] - u["logits_per_text"]).abs().max().item() < tol

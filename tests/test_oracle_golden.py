@@ -129,3 +129,12 @@ def test_tiny_gradients(golden, tag, adapters):
         ref = g["grad/" + n]
         scale = max(1e-3, float(np.abs(ref).max()))
         np.testing.assert_allclose(t.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=n)
+
+
+@pytest.mark.parametrize("tag", ["sq", "crop"])
+def test_image_processor_matches_hf(golden, tag):
+    """oracle.image_processor vs transformers' CLIPImageProcessor (OpenAI defaults, no resize)."""
+    g = golden("image_processor.npz")
+    out = R.image_processor(g[f"{tag}_images"], 224, g["mean"], g["std"])
+    assert out.shape == g[f"{tag}_pixel_values"].shape
+    assert np.abs(out - g[f"{tag}_pixel_values"]).max() < 1e-5

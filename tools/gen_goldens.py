@@ -211,8 +211,35 @@ def gen_quirks():
     print("Q3 error:", err)
 
 
+def gen_image_processor():
+    """The input step: the reference gets pixel_values from
+    CLIPProcessor.from_pretrained(...) (model_m.py:30, dataset.py:152-164), i.e. transformers'
+    CLIPImageProcessor with OpenAI CLIP's defaults.  Built here with those defaults (no hub),
+    resize off (the fused GPU step covers center_crop + rescale + normalize): a 224x224 image
+    and a 240x256 one that exercises the centre crop."""
+    from transformers import CLIPImageProcessor
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        proc = CLIPImageProcessor()
+    rng = np.random.default_rng(2024)
+    out = {}
+    for tag, (h, w) in (("sq", (224, 224)), ("crop", (240, 256))):
+        img = rng.integers(0, 256, (1, h, w, 3), dtype=np.uint8)
+        pv = proc(images=list(img), return_tensors="np", do_resize=False, do_center_crop=True)["pixel_values"]
+        out[f"{tag}_images"] = img
+        out[f"{tag}_pixel_values"] = pv
+    out["mean"] = np.array(proc.image_mean, dtype=np.float64)
+    out["std"] = np.array(proc.image_std, dtype=np.float64)
+    save("image_processor.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1:  # named generators only
+        for name in sys.argv[1:]:
+            globals()[f"gen_{name}"]()
+        sys.exit(0)
     gen_checkpoint_schema()
     gen_quirks()
     gen_adapters()

@@ -68,6 +68,23 @@ _lib.declare("clipmi_text_embed", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c
 _lib.declare("clipmi_text_embed_bwd_ws", [c_int, c_int], c_i64)
 _lib.declare("clipmi_text_embed_bwd", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64])
 _lib.declare("clipmi_im2col", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
+_lib.declare("clipmi_im2col_u8", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  ctypes.POINTER(c_float), ctypes.POINTER(c_float)])
+
+# CLIPImageProcessor defaults (OpenAI CLIP, [HF] utils/constants.py: OPENAI_CLIP_MEAN / _STD)
+IMAGE_MEAN = (0.48145466, 0.4578275, 0.40821073)
+IMAGE_STD = (0.26862954, 0.26130258, 0.27577711)
+
+
+def im2col_uint8(images, X, image_size, patch, mean=IMAGE_MEAN, std=IMAGE_STD):
+    """uint8 images [B, H, W, 3] (channels last, H, W >= image_size) -> normalised im2col rows
+    in X [B*(G*G+1), 3*P*P]: CLIPImageProcessor's center_crop + rescale + normalize fused into
+    patch-embed's im2col (one kernel, 1 B read per pixel value instead of 4)."""
+    B, H, W, C = images.shape
+    m = (c_float * 3)(*mean)
+    sd = (c_float * 3)(*std)
+    call("clipmi_im2col_u8", K.stream(), dcode(X.dtype), P_(images), P_(X), B, H, W, image_size, patch,
+         X.shape[1], m, sd)
 _lib.declare("clipmi_pool_index", [c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp])
 _lib.declare("clipmi_gather_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp])
 _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int])
@@ -194,13 +211,21 @@ class VisionTowerFn(torch.autograd.Function):
         rt = runtime
         arena, v, dtype = rt.arena, rt.cfg.vision_config, rt.dtype
         B = pixel_values.shape[0]
-        if pixel_values.dim() != 4 or pixel_values.shape[1] != v.num_channels:
-            raise ValueError(f"pixel_values must be [B, {v.num_channels}, H, W]")
-        H, W = pixel_values.shape[2], pixel_values.shape[3]
-        if H != v.image_size or W != v.image_size:
-            raise ValueError(f"Input image size ({H}*{W}) doesn't match model ({v.image_size}*{v.image_size}).")
+        raw = pixel_values.dtype == torch.uint8  # decoded images, channels last: fused input step
+        if raw:
+            if pixel_values.dim() != 4 or pixel_values.shape[3] != v.num_channels:
+                raise ValueError(f"uint8 images must be [B, H, W, {v.num_channels}] (channels last)")
+            H, W = pixel_values.shape[1], pixel_values.shape[2]
+            if H < v.image_size or W < v.image_size:
+                raise ValueError(f"uint8 images ({H}*{W}) are smaller than the crop ({v.image_size}); resize first")
+        else:
+            if pixel_values.dim() != 4 or pixel_values.shape[1] != v.num_channels:
+                raise ValueError(f"pixel_values must be [B, {v.num_channels}, H, W]")
+            H, W = pixel_values.shape[2], pixel_values.shape[3]
+            if H != v.image_size or W != v.image_size:
+                raise ValueError(f"Input image size ({H}*{W}) doesn't match model ({v.image_size}*{v.image_size}).")
         dev = pixel_values.device
-        px = pixel_values.to(torch.float32).contiguous()
+        px = pixel_values.contiguous() if raw else pixel_values.to(torch.float32).contiguous()
         N, D, Pp = v.num_positions, v.hidden_size, v.patch_size
         Kp = v.num_channels * Pp * Pp
         if Kp % 8:
@@ -211,7 +236,10 @@ class VisionTowerFn(torch.autograd.Function):
         wbuf = _wbuf(arena, dtype)
         dc = dcode(dtype)
         X = torch.empty(R, Kp, dtype=dtype, device=dev)
-        call("clipmi_im2col", s, dc, P_(px), P_(X), B, v.num_channels, H, Pp, Kp)
+        if raw:
+            im2col_uint8(px, X, v.image_size, Pp)
+        else:
+            call("clipmi_im2col", s, dc, P_(px), P_(X), B, v.num_channels, H, Pp, Kp)
         h0 = torch.empty(R, D, dtype=dtype, device=dev)
         K.gemm(R, D, Kp, X, Kp, True, arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kp),
                Kp, True, h0, D)

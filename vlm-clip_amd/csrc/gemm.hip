@@ -802,20 +802,29 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
       }
 #pragma unroll
       for (int i = 0; i < MPH; ++i) fa[i] = read_frag_pp<AK>(img, wm * 128 + (ph * MPH + i) * 16, lane);
-      if (issue) {
+      constexpr bool DMA_IN_MFMA = PPV & 16;  // issue the DMAs between this phase's MFMAs
+      if (issue && !DMA_IN_MFMA) {
         if (NPH == 1 || ph == 0) stage_pp<AK>(slot(st + PP_D), A, p.lda, m0, p.M, kn, kend, wave, lane);
         if (NPH == 1 || ph == 1) stage_pp<BKM>(slot(st + PP_D) + 16384, B, p.ldb, n0, p.N, kn, kend, wave, lane);
       }
-      if (ph == NPH - 1) pp_vmcnt(4 * max(0, min(PP_D - 1, ns - st - 2)));  // stage st + 1 landed
+      if (ph == NPH - 1) {  // stage st + 1 landed (with DMA_IN_MFMA this phase's own 2 are not issued yet)
+        if (DMA_IN_MFMA && issue) pp_vmcnt(4 * (PP_D - 1) - 2);
+        else pp_vmcnt(4 * max(0, min(PP_D - 1, ns - st - 2)));
+      }
       pp_barrier();
       // ---- MFMA section
       if (!(PPV & 4)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < MPH; ++i)
+      for (int i = 0; i < MPH; ++i) {
+        if (DMA_IN_MFMA && issue && i == MPH / 2) {
+          if (NPH == 1 || ph == 0) stage_pp<AK>(slot(st + PP_D), A, p.lda, m0, p.M, kn, kend, wave, lane);
+          if (NPH == 1 || ph == 1) stage_pp<BKM>(slot(st + PP_D) + 16384, B, p.ldb, n0, p.N, kn, kend, wave, lane);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[ph * MPH + i][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[ph * MPH + i][j], 0, 0, 0);
+      }
       if (BIASGRAD && do_bias) {
 #pragma unroll
         for (int h = 0; h < MPH / 4; ++h) {
@@ -1252,6 +1261,8 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
     case 4: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
     case 9: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
     case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); break;  // no epilogue (timing)
+    case 13: launch_ppv<AK, BKM, OutT, EPI, BG, 16>(p, splits, s, bias_grad); break;  // DMAs between MFMAs
+    case 14: launch_ppv<AK, BKM, OutT, EPI, BG, 20>(p, splits, s, bias_grad); break;  // + no setprio
 #ifdef CLIPMI_GEMM_EXPERIMENTS
     case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
     case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
