@@ -44,57 +44,80 @@ __device__ __forceinline__ void vstore(T* p, const float* o) {
 
 // y = LN(x [+ pos[row % period] + (row % period == 0 ? cls : 0)]) * w + b
 // When pos is given the pre-LN sum is written back to x (the vision embedding output).
+// A wave normalises LN_RPW rows, issuing every row's loads before the first reduction so
+// twice the bytes are in flight per wave (one row per wave ran at 4.2 TB/s, latency bound).
+constexpr int LN_RPW = 2;
+
 template <typename T, int PS, int NP>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
                                                      float* mean_out, float* rstd_out, int R, int D, float eps,
                                                      const T* pos, const T* cls, int period) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= R) return;
-  T* xr = x + (int64_t)row * ldx;
-  float v[NP][PS];
-  float s = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_RPW;
+  if (row0 >= R) return;
+  float v[LN_RPW][NP][PS];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int c = (k * 64 + lane) * PS;
-    vload<T, PS>(xr + c, v[k]);
-    if (pos) {
-      const int t = row % period;
-      float pv[PS];
-      vload<T, PS>(pos + (int64_t)t * D + c, pv);
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const int row = min(row0 + rr, R - 1);  // a tail wave recomputes row R-1 and does not store it twice
+    T* xr = x + (int64_t)row * ldx;
 #pragma unroll
-      for (int j = 0; j < PS; ++j) v[k][j] += pv[j];
-      if (cls && t == 0) {
-        vload<T, PS>(cls + c, pv);
-#pragma unroll
-        for (int j = 0; j < PS; ++j) v[k][j] += pv[j];
-      }
-      vstore<T, PS>(xr + c, v[k]);
-    }
-#pragma unroll
-    for (int j = 0; j < PS; ++j) s += v[k][j];
+    for (int k = 0; k < NP; ++k) vload<T, PS>(xr + (k * 64 + lane) * PS, v[rr][k]);
   }
-  const float mean = wave_sum(s) / D;
-  float q = 0.f;
+  float mean[LN_RPW], rstd[LN_RPW];
 #pragma unroll
-  for (int k = 0; k < NP; ++k)
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const int row = min(row0 + rr, R - 1);
+    const bool own = row0 + rr < R;
+    float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < PS; ++j) { float d = v[k][j] - mean; q += d * d; }
-  const float rstd = rsqrtf(wave_sum(q) / D + eps);
-  T* yr = y + (int64_t)row * ldy;
+    for (int k = 0; k < NP; ++k) {
+      const int c = (k * 64 + lane) * PS;
+      if (pos) {
+        const int t = row % period;
+        float pv[PS];
+        vload<T, PS>(pos + (int64_t)t * D + c, pv);
+#pragma unroll
+        for (int j = 0; j < PS; ++j) v[rr][k][j] += pv[j];
+        if (cls && t == 0) {
+          vload<T, PS>(cls + c, pv);
+#pragma unroll
+          for (int j = 0; j < PS; ++j) v[rr][k][j] += pv[j];
+        }
+        if (own) vstore<T, PS>(x + (int64_t)row * ldx + c, v[rr][k]);
+      }
+#pragma unroll
+      for (int j = 0; j < PS; ++j) s += v[rr][k][j];
+    }
+    mean[rr] = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+      for (int j = 0; j < PS; ++j) { const float d = v[rr][k][j] - mean[rr]; q += d * d; }
+    rstd[rr] = rsqrtf(wave_sum(q) / D + eps);
+  }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int c = (k * 64 + lane) * PS;
-    float wv[PS], bv[PS], o[PS];
+    float wv[PS], bv[PS];
     vload<T, PS>(w + c, wv);
     vload<T, PS>(b + c, bv);
 #pragma unroll
-    for (int j = 0; j < PS; ++j) o[j] = (v[k][j] - mean) * rstd * wv[j] + bv[j];
-    vstore<T, PS>(yr + c, o);
+    for (int rr = 0; rr < LN_RPW; ++rr) {
+      if (row0 + rr >= R) continue;
+      float o[PS];
+#pragma unroll
+      for (int j = 0; j < PS; ++j) o[j] = (v[rr][k][j] - mean[rr]) * rstd[rr] * wv[j] + bv[j];
+      vstore<T, PS>(y + (int64_t)(row0 + rr) * ldy + c, o);
+    }
   }
   if (lane == 0) {
-    if (mean_out) mean_out[row] = mean;
-    if (rstd_out) rstd_out[row] = rstd;
+#pragma unroll
+    for (int rr = 0; rr < LN_RPW; ++rr) {
+      if (row0 + rr >= R) continue;
+      if (mean_out) mean_out[row0 + rr] = mean[rr];
+      if (rstd_out) rstd_out[row0 + rr] = rstd[rr];
+    }
   }
 }
 
@@ -378,7 +401,7 @@ __global__ __launch_bounds__(256) void id_chunk_sum_kernel(const int* perm, cons
 template <typename T, int PS, int NP>
 void ln_fwd_launch(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, const void* w, const void* b,
                    float* mean, float* rstd, int R, int D, float eps, const void* pos, const void* cls, int period) {
-  hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP>), dim3((R + 3) / 4), dim3(256), 0, s, (T*)x, ldx, (T*)y, ldy,
+  hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s, (T*)x, ldx, (T*)y, ldy,
                      (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const T*)pos, (const T*)cls, period);
 }
 template <typename T, int PS, int NP>
