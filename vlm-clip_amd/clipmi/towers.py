@@ -122,6 +122,18 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+def _gemm_f32(M, N, Kd, A, lda, akm, B, ldb, bkm, C, ldc, flags=0):
+    """fp32 GEMM (the contrastive similarities and their gradients) split over K when its
+    64x64 tiles would not fill two rounds of the CUs: at one GPU (B = Bg = 1024) the backward
+    products have 128 tiles for 256 CUs."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    split = 1
+    while split < 8 and tiles * split * 2 <= 512 and Kd // (split * 2) >= 128:
+        split *= 2
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=C.device) if split > 1 else None
+    K.gemm(M, N, Kd, A, lda, akm, B, ldb, bkm, C, ldc, flags=flags, split_k=split, workspace=ws)
+
+
 # ------------------------------------------------------------------------------ encoder
 class Encoder:
     """Binds one tower's encoder layers (an arena prefix) to the native engine."""
@@ -566,8 +578,8 @@ class ContrastiveFn(torch.autograd.Function):
         Bg = tg.shape[0]
         lt = torch.empty(B, Bg, dtype=torch.float32, device=dev)
         li = torch.empty(B, Bg, dtype=torch.float32, device=dev)
-        K.gemm(B, Bg, E, th, E, True, ig, E, True, lt, Bg)   # cos(t_local, i_all)
-        K.gemm(B, Bg, E, ih, E, True, tg, E, True, li, Bg)   # cos(i_local, t_all)
+        _gemm_f32(B, Bg, E, th, E, True, ig, E, True, lt, Bg)   # cos(t_local, i_all)
+        _gemm_f32(B, Bg, E, ih, E, True, tg, E, True, li, Bg)   # cos(i_local, t_all)
         lse = torch.empty(2, B, dtype=torch.float32, device=dev)
         ce = torch.empty(2, B, dtype=torch.float32, device=dev)
         ls = logit_scale.detach().reshape(1)
@@ -607,12 +619,12 @@ class ContrastiveFn(torch.autograd.Function):
         # accumulate on top through the GEMM's beta epilogue
         dTg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
         dIg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
-        K.gemm(Bg, E, B, dSi, Bg, False, ih, E, False, dTg, E)
-        K.gemm(Bg, E, B, dSt, Bg, False, th, E, False, dIg, E)
+        _gemm_f32(Bg, E, B, dSi, Bg, False, ih, E, False, dTg, E)
+        _gemm_f32(Bg, E, B, dSt, Bg, False, th, E, False, dIg, E)
         dth = _reduce_scatter(dTg, ctx.group, world)
         dih = _reduce_scatter(dIg, ctx.group, world)
-        K.gemm(B, E, Bg, dSt, Bg, True, ig, E, False, dth, E, flags=_lib.EPI_BETA)
-        K.gemm(B, E, Bg, dSi, Bg, True, tg, E, False, dih, E, flags=_lib.EPI_BETA)
+        _gemm_f32(B, E, Bg, dSt, Bg, True, ig, E, False, dth, E, flags=_lib.EPI_BETA)
+        _gemm_f32(B, E, Bg, dSi, Bg, True, tg, E, False, dih, E, flags=_lib.EPI_BETA)
         if gth is not None:
             dth += gth
         if gih is not None:
