@@ -517,15 +517,116 @@ __device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4]
   }
 }
 
+// Full-line stores through LDS: the values of epilogue256_w (same math, same loads) are written
+// to the wave's 16 KiB LDS region as a [128 rows][64 cols] bf16 tile (16-B chunk c of row r at
+// c ^ (r & 7): conflict-free 8-lane writes and 16-lane reads), then read back row-contiguous so
+// each global store instruction covers 8 whole 128-B rows instead of 16 rows x 64 B.  Needs
+// the ring idle (after the kernel's final barrier) and is used for the pre-activation store too.
+__device__ __forceinline__ int stage_off(int r, int c8) { return r * 128 + ((c8 ^ (r & 7)) << 4); }
+
+__device__ __forceinline__ void stage_store_rows(const GemmP& p, const char* st, bf16* out, int64_t ld, int mb, int nb,
+                                                 int lane) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {  // 64 rows, 8 whole rows per instruction
+    const int r = it * 8 + (lane >> 3), c8 = lane & 7;
+    const u32x4 v = *LDS_PTR(const u32x4, st + stage_off(r, c8));
+    const int m = mb + r, n = nb + c8 * 8;
+    if (m < p.M && n < p.N) *(u32x4*)(out + (int64_t)m * ld + n) = v;
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane,
+                                                char* st) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
+  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
+  constexpr bool HAUX = HDQ || HDG;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);
+  char* st_out = st;           // [64 rows][64 cols] bf16 = 8 KiB per half of the wave's rows
+  char* st_pre = st + 8192;
+  float bv[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const int n = min(nb + 32 * jp + coff, p.N - 8);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) {
+        load4((const float*)p.bias + n, bv[jp]);
+        load4((const float*)p.bias + n + 4, bv[jp] + 4);
+      } else {
+        load8((const bf16*)p.bias + n, bv[jp]);
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float xin[4][2][8];
+    if (HR || HAUX || HBETA) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int n = min(nb + 32 * jp + coff, p.N - 8);
+          if (HR) load8((const bf16*)p.res + (int64_t)m * p.ldr + n, xin[ii][jp]);
+          else if (HAUX) load8((const bf16*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][jp]);
+          else load8((const bf16*)p.C + (int64_t)m * p.ldc + n, xin[ii][jp]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = h * 4 + ii;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
+          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+        }
+        const int off = stage_off(ii * 16 + mlane, (32 * jp + coff) >> 3);
+        if (HPRE)
+          *LDS_PTR(bf16x8, st_pre + off) = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
+                                                  (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (HQ) v[r] = quick_gelu(v[r]);
+          if (HG) v[r] = gelu_erf(v[r]);
+          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][jp][r]);
+          if (HDG) v[r] *= gelu_erf_grad(xin[ii][jp][r]);
+          if (HR || HBETA) v[r] += xin[ii][jp][r];
+        }
+        *LDS_PTR(bf16x8, st_out + off) = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
+                                                (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staging writes landed
+    if (HPRE) stage_store_rows(p, st_pre, (bf16*)p.aux, p.ldaux, mb + h * 64, nb, lane);
+    stage_store_rows(p, st_out, (bf16*)p.C, p.ldc, mb + h * 64, nb, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next half overwrites
+  }
+}
+
 // Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
 // allows it (4-aligned columns, aligned leading dims; the 16-B form for bf16 output when
 // columns, leading dims and pointers allow 16-B accesses), else the per-subtile generic path
 // (split-K slab kz, ragged N, runtime flags).
 template <typename OutT, int EPI>
-__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane, int kz) {
+__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane, int kz,
+                                          char* stage = nullptr) {
   constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
                         !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
   if constexpr (FAST && std::is_same<OutT, bf16>::value) {
+    if (stage && !p.ws && p.vec8) {
+      epilogue256_lds<EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane, stage);
+      return;
+    }
     if (!p.ws && p.vec8) {
       epilogue256_w<EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
       return;
@@ -852,7 +953,12 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
     return;
   }
-  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz);
+  // bf16 stores through LDS, whole 128-B rows per instruction (the ring is idle: every wave has
+  // passed its last MFMA section and the trailing barrier above pairs the two groups).  Not for
+  // the two-output fc1 epilogue, whose direct stores overlap its gelu math better (measured);
+  // PPV & 32 forces it, PPV & 64 disables it (A/B hooks).
+  constexpr bool STAGE = (PPV & 32) || (!(PPV & 64) && EPI >= 0 && !(EPI & CLIPMI_EPI_STORE_PRE));
+  finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz, STAGE ? smem + wave * 16384 : nullptr);
 }
 
 // ------------------------------------------------------------------ persistent ping-pong
@@ -1263,6 +1369,8 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
     case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); break;  // no epilogue (timing)
     case 13: launch_ppv<AK, BKM, OutT, EPI, BG, 16>(p, splits, s, bias_grad); break;  // DMAs between MFMAs
     case 14: launch_ppv<AK, BKM, OutT, EPI, BG, 20>(p, splits, s, bias_grad); break;  // + no setprio
+    case 15: launch_ppv<AK, BKM, OutT, EPI, BG, 32>(p, splits, s, bias_grad); break;  // stores through LDS
+    case 16: launch_ppv<AK, BKM, OutT, EPI, BG, 64>(p, splits, s, bias_grad); break;  // direct stores only
 #ifdef CLIPMI_GEMM_EXPERIMENTS
     case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
     case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
