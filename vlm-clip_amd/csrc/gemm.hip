@@ -544,8 +544,7 @@ __device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][
   constexpr bool HAUX = HDQ || HDG;
   const int q = lane >> 4, mlane = lane & 15;
   const int coff = 16 * (q & 1) + 8 * (q >> 1);
-  char* st_out = st;           // [64 rows][64 cols] bf16 = 8 KiB per half of the wave's rows
-  char* st_pre = st + 8192;
+  char* st_out = st;  // [64 rows][64 cols] bf16 = 8 KiB per half of the wave's rows
   float bv[2][8];
 #pragma unroll
   for (int jp = 0; jp < 2; ++jp) {
@@ -591,9 +590,10 @@ __device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][
           v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
         }
         const int off = stage_off(ii * 16 + mlane, (32 * jp + coff) >> 3);
-        if (HPRE)
-          *LDS_PTR(bf16x8, st_pre + off) = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
-                                                  (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+        if (HPRE) {  // the pre-activation goes out directly (16 rows x 64 B), overlapping the gelu math
+          const int m = mb + i * 16 + mlane, n = nb + 32 * jp + coff;
+          if (m < p.M && n < p.N) store8((bf16*)p.aux + (int64_t)m * p.ldaux + n, v);
+        }
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           if (HQ) v[r] = quick_gelu(v[r]);
@@ -607,7 +607,6 @@ __device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staging writes landed
-    if (HPRE) stage_store_rows(p, st_pre, (bf16*)p.aux, p.ldaux, mb + h * 64, nb, lane);
     stage_store_rows(p, st_out, (bf16*)p.C, p.ldc, mb + h * 64, nb, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next half overwrites
   }
@@ -954,10 +953,9 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
     return;
   }
   // bf16 stores through LDS, whole 128-B rows per instruction (the ring is idle: every wave has
-  // passed its last MFMA section and the trailing barrier above pairs the two groups).  Not for
-  // the two-output fc1 epilogue, whose direct stores overlap its gelu math better (measured);
-  // PPV & 32 forces it, PPV & 64 disables it (A/B hooks).
-  constexpr bool STAGE = (PPV & 32) || (!(PPV & 64) && EPI >= 0 && !(EPI & CLIPMI_EPI_STORE_PRE));
+  // passed its last MFMA section and the trailing barrier above pairs the two groups).  fc1's
+  // pre-activation still goes out directly, beside its gelu math.  PPV & 64 disables it (A/B).
+  constexpr bool STAGE = (PPV & 32) || (!(PPV & 64) && EPI >= 0);
   finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz, STAGE ? smem + wave * 16384 : nullptr);
 }
 
