@@ -34,6 +34,9 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("sq4k", 4096, 4096, 4096, True, True, torch.bfloat16, 0, 1),
     ("sq8k", 8192, 8192, 8192, True, True, torch.bfloat16, 0, 1),
 ]
+if os.environ.get("GEMM_SPLITS"):  # GEMM_SPLITS=7,9,28: each wgrad shape once per explicit split (+ reduce)
+    SHAPES = [sh[:-1] + (sp,) if sh[-1] == 2 else sh
+              for sh in SHAPES for sp in ([int(x) for x in os.environ["GEMM_SPLITS"].split(",")] if sh[-1] == 2 else [0])]
 VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,10").split(",")]
 REPS = int(os.environ.get("GEMM_REPS", "10"))
 only = sys.argv[1:] if len(sys.argv) > 1 else None
@@ -64,16 +67,20 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     bias = torch.randn(N, device="cuda").to(torch.bfloat16)
     aux = torch.randn(M, N, device="cuda").to(odt) if flags & (_lib.EPI_DQGELU | _lib.EPI_STORE_PRE) else None
     res = torch.randn(M, N, device="cuda").to(odt) if flags & _lib.EPI_RESID else None
-    if split == 2:  # engine.cpp wgrad_splits: the smallest split filling whole rounds of 256 CUs best
+    if split == 2:  # engine.cpp wgrad_splits: round efficiency minus the slabs' cost
         tiles = ((M + 255) // 256) * ((N + 255) // 256)
-        split, best = 1, 0.0
+        compute = 2.0 * M * N * Kd / (4.1e12 * 256)
+        split, best = 1, -1e30
         for sp in range(1, 65):
             if sp > 1 and Kd // sp < 512:
                 break
             wg = tiles * sp
             eff = wg / (256 * ((wg + 255) // 256))
-            if eff > best + 0.02:
-                split, best = sp, eff
+            score = eff - (2.0 * sp * M * N * 4 / 4.0e12 if sp > 1 else 0.0) / compute
+            if score > best + 0.005:
+                split, best = sp, score
+    if split == 0:
+        continue
     ws = torch.empty(split * M * N, device="cuda") if split > 1 else None
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,

@@ -67,10 +67,12 @@ int cu_count() {
 }
 
 // split-K factor for a wgrad GEMM [M x N] reducing over K tokens.  bf16 (256x256 tiles, one
-// workgroup per CU): the smallest split whose workgroups fill whole rounds of the chip best,
-// with >= 512 tokens per slab.  ViT-B/16 out-proj (768x768 = 9 tiles): 28 splits = 252
-// workgroups in one round, where a fixed 512-workgroup target gave 32 = 288, a second round
-// 1/8 full; text out-proj (4 tiles): 64 splits instead of 32 that left half the chip idle.
+// workgroup per CU): the split maximising round efficiency (workgroups / whole rounds of the
+// chip's CUs) minus the fp32 slabs' cost (written by the GEMM, read back by the reduce) relative
+// to the GEMM's compute time, with >= 512 tokens per slab.  Measured on ViT-B/16 B=1024
+// (tools/gemm_bench.py GEMM_SPLITS): qkv (27 tiles) 9 splits = 243 workgroups in one round,
+// 676 us, vs 28 splits (756 in three rounds, 3x the slab bytes) 732 us; fc1/fc2 (36 tiles) 7;
+// out-proj (9 tiles) 28; text out-proj (4 tiles) 64.
 int wgrad_splits(int M, int N, int K, int dt) {
   const int tile = dt == CLIPMI_BF16 ? 256 : 64;
   const int tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
@@ -81,16 +83,19 @@ int wgrad_splits(int M, int N, int K, int dt) {
     return s;
   }
   const int cus = cu_count();
+  const double compute_s = 2.0 * M * N * (double)K / (4.1e12 * cus);  // ~1.05 PF/s on 256 CUs
   int best = 1;
-  double best_eff = 0.0;
+  double best_score = -1e30;
   for (int s = 1; s <= 64; ++s) {
     if (s > 1 && (int64_t)K / s < 512) break;
     const int64_t wg = (int64_t)tiles * s;
     const int64_t rounds = (wg + cus - 1) / cus;
     const double eff = (double)wg / (double)(rounds * cus);
-    if (eff > best_eff + 0.02) {
+    const double slab_s = s > 1 ? 2.0 * s * M * N * 4.0 / 4.0e12 : 0.0;  // fp32 slabs out + in, ~4 TB/s
+    const double score = eff - slab_s / compute_s;
+    if (score > best_score + 0.005) {
       best = s;
-      best_eff = eff;
+      best_score = score;
     }
   }
   return best;

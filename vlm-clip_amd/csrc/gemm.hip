@@ -1284,6 +1284,41 @@ __global__ void splitk_reduce_kernel(const float* ws, float* C, int64_t ldc, int
   }
 }
 
+// same reduction, four columns per lane and eight slabs' loads in flight before the (fixed-order)
+// adds: the scalar loop above waits one HBM round trip per slab.  N % 4 == 0, ldc % 4 == 0.
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* ws, float* C, int64_t ldc, int M, int N,
+                                                             int splits, float alpha, int beta) {
+  const int64_t total = (int64_t)M * N;
+  const int n4 = N >> 2;
+  const int64_t total4 = (int64_t)M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+    const float* src = ws + (int64_t)m * N + n;
+    float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const float4*)(src + (int64_t)(z + j) * total);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sum.x += v[j].x; sum.y += v[j].y; sum.z += v[j].z; sum.w += v[j].w;
+      }
+    }
+    for (; z < splits; ++z) {
+      const float4 v = *(const float4*)(src + (int64_t)z * total);
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    float4* c = (float4*)(C + (int64_t)m * ldc + n);
+    float4 r = make_float4(alpha * sum.x, alpha * sum.y, alpha * sum.z, alpha * sum.w);
+    if (beta) {
+      const float4 o = *c;
+      r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    }
+    *c = r;
+  }
+}
+
 template <bool AK, bool BKM, typename OutT, int EPI>
 void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OutT, EPI>), dim3(p.ntiles, splits), dim3(NTHR), 65536, s, p);
@@ -1569,10 +1604,16 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   CLIPMI_CHECK_LAUNCH();
   if (p.ws) {
     const int64_t total = (int64_t)d->M * d->N;
-    const unsigned nblk = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
-                       p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha,
-                       (d->flags & CLIPMI_EPI_BETA) ? 1 : 0);
+    const int beta = (d->flags & CLIPMI_EPI_BETA) ? 1 : 0;
+    if (d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0 && ((uintptr_t)p.ws & 15) == 0) {
+      const unsigned nblk = (unsigned)std::min<int64_t>((total / 4 + 255) / 256, 65536);
+      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(nblk), dim3(256), 0, s,
+                         p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta);
+    } else {
+      const unsigned nblk = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
+                         p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta);
+    }
     CLIPMI_CHECK_LAUNCH();
   }
   return CLIPMI_OK;

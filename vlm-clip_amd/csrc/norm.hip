@@ -218,6 +218,64 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* ws, 
   }
 }
 
+// the same sum over up to two column ranges at once: columns [0, D) -> out, [D, 2D) -> out2
+// (out2 may be null: grid covers D columns only).  16 lanes x 4 columns per partial group,
+// 64 groups, eight loads in flight per lane, fixed-order LDS tree: the one-float-per-lane
+// kernel above waits ~P/32 HBM round trips on only D/64 workgroups (43 us at P=1024, D=768).
+// D % 4 == 0, stride % 4 == 0, ws 16-B aligned.
+__global__ __launch_bounds__(1024) void reduce_partials4_kernel(const float* ws, int64_t stride, int P, int D,
+                                                                float* out, float* out2, int beta) {
+  __shared__ float4 red[64][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + tx * 4;
+  const int Dt = out2 ? 2 * D : D;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < Dt) {
+    const float* src = ws + c;
+    int p = ty;
+    for (; p + 7 * 64 < P; p += 8 * 64) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const float4*)(src + (int64_t)(p + j * 64) * stride);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
+      }
+    }
+    for (; p < P; p += 64) {
+      const float4 v = *(const float4*)(src + (int64_t)p * stride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[ty][tx] = acc;
+  __syncthreads();
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ty < 16) {
+    a = red[ty * 4][tx];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 b = red[ty * 4 + k][tx];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  __syncthreads();
+  if (ty < 16) red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < Dt) {
+    float4 t = red[0][tx];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      const float4 b = red[k][tx];
+      t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+    }
+    float* o = c < D ? out + c : out2 + (c - D);
+    if (beta) {
+      t.x += o[0]; t.y += o[1]; t.z += o[2]; t.w += o[3];
+    }
+    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+  }
+}
+
 // column partial sums of a [R, N] matrix: ws[chunk][N], chunk = blockIdx.y
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* x, int64_t ldx, int R, int N, int rows_per,
@@ -465,8 +523,15 @@ extern "C" int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int
   if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
   else LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
   CLIPMI_CHECK_LAUNCH();
-  if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
-  if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
+  if (((uintptr_t)wsf & 15) != 0) {
+    if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
+    if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
+  } else if (dw && db)
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, db, beta_wb);
+  else if (dw)
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, (float*)nullptr, beta_wb);
+  else if (db)
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, (float*)nullptr, beta_wb);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
@@ -491,7 +556,10 @@ extern "C" int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx
   dim3 g((N / 4 + 255) / 256, chunks);
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, R, N, rows_per, (float*)ws);
   else hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, R, N, rows_per, (float*)ws);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
+  if (((uintptr_t)ws & 15) == 0)
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, (float*)nullptr, beta);
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
