@@ -112,7 +112,7 @@ int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx,
 int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* dst,
                         int beta);
 
-/* ---- Attention (head_dim 64, N <= 256) ([HF] CLIPAttention :298-335, eager core :259-277) -----
+/* ---- Attention (head_dim 64, N <= 288) ([HF] CLIPAttention :298-335, eager core :259-277) -----
  * qkv: [B*N, 3D] (q | k | v, head h at h*64), o: [B*N, D], lse: [B*H*N] fp32.
  * attention_mask: int64 [B, N] key padding (1 keep) or NULL; causal for the text tower. */
 int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse, const int64_t* attention_mask,

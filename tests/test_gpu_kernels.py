@@ -95,6 +95,8 @@ def attn_ref(qkv, B, N, H, mask, causal):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 50, 12, False), (2, 197, 12, False),
                                            (3, 77, 8, True), (2, 256, 2, False),
+                                           # ViT-L/14 at 224 (N = 257) and the N <= 288 limit
+                                           (2, 257, 16, False), (3, 288, 2, False), (40, 257, 16, False),
                                            # more (batch, head) items than the persistent grid
                                            (90, 197, 12, False), (130, 77, 8, True)])
 def test_attention(dtype, B, N, H, causal):
@@ -160,16 +162,19 @@ def test_text_embedding_fwd_bwd(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_im2col_matches_conv(dtype):
-    B, H, P, D = 2, 64, 16, 128
+@pytest.mark.parametrize("H,P", [(64, 16), (56, 14)])  # P=14 (ViT-L/14): K = 588 padded to 640
+def test_im2col_matches_conv(dtype, H, P):
+    B, D = 2, 128
     px = rnd((B, 3, H, H), 18)
     W = rnd((D, 3, P, P), 19, scale=0.05)
     G = H // P
-    Kp = 3 * P * P
+    Kc = 3 * P * P
+    Kp = (Kc + 63) // 64 * 64 if Kc % 8 else Kc
     X = torch.empty(B * (G * G + 1), Kp, dtype=dtype, device="cuda")
     T.call("clipmi_im2col", kern.stream(), DT[dtype], px.data_ptr(), X.data_ptr(), B, 3, H, P, Kp)
+    assert X[:, Kc:].abs().max().item() == 0 if Kp > Kc else True
     out = torch.empty(B * (G * G + 1), D, dtype=torch.float32, device="cuda")
-    Wd = W.to(dtype).view(D, Kp).contiguous()
+    Wd = F.pad(W.to(dtype).view(D, Kc), (0, Kp - Kc)).contiguous()
     kern.gemm(B * (G * G + 1), D, Kp, X, Kp, True, Wd, Kp, True, out, D)
     ref = F.conv2d(px, W, stride=P).flatten(2).transpose(1, 2)
     out = out.view(B, G * G + 1, D)

@@ -38,7 +38,9 @@ def make(preset, adapters, precision, freeze=True):
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("tag,preset,B,adapters", [("tiny", "tiny", 4, True), ("b32", "B/32", 8, True),
                                                    ("b32_noadapter", "B/32", 8, False),
-                                                   ("b16", "B/16", 4, False)])
+                                                   ("b16", "B/16", 4, False),
+                                                   # config 4's model: P=14 (patch K 588 -> 640), N=257
+                                                   ("l14", "L/14", 2, True)])
 def test_forward_matches_reference(golden, precision, tag, preset, B, adapters):
     g = golden(f"forward_{tag}.npz")
     m = make(preset, adapters, precision)
@@ -68,11 +70,19 @@ def test_eos_pooling_fp32(golden):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-@pytest.mark.parametrize("tag,adapters,freeze", [("tiny_adapter_grads", True, True), ("tiny_full_grads", False, False)])
-def test_gradients_match_reference(golden, precision, tag, adapters, freeze):
+@pytest.mark.parametrize("tag,preset,B,adapters,freeze", [("tiny_adapter_grads", "tiny", 4, True, True),
+                                                          ("tiny_full_grads", "tiny", 4, False, False),
+                                                          ("l14", "L/14", 2, True, True)])
+def test_gradients_match_reference(golden, precision, tag, preset, B, adapters, freeze):
+    if preset != "tiny" and precision == "bf16":
+        # B=2 with near-saturated softmax: d loss/d logit = p - y is a small difference of
+        # O(1) terms, so bf16's ~0.12 logit error (checked by test_forward_matches_reference)
+        # moves it by tens of percent whatever the kernels do; the bf16 backward arithmetic
+        # is pinned by the tiny cases, the L/14 shapes by the fp32 case
+        pytest.skip("ill-conditioned at B=2 in bf16; see comment")
     g = golden(f"forward_{tag}.npz")
-    m = make("tiny", adapters, precision, freeze=freeze)
-    out = m(**batch(m.config, 4, g))
+    m = make(preset, adapters, precision, freeze=freeze)
+    out = m(**batch(m.config, B, g))
     out["loss"].backward()
     torch.cuda.synchronize()
     assert abs(out["loss"].item() - float(g["loss"])) < (1e-5 if precision == "fp32" else 2e-2)
@@ -94,7 +104,9 @@ def test_gradients_match_reference(golden, precision, tag, adapters, freeze):
     print(f"\n[{tag} {precision}] worst grad err {worst[0]:.3e} at {worst[1]}")
     # bf16 mode stores activation gradients in bf16 (pooled-row gradient cast, LN backward
     # cancellation): measured worst 0.14 on the adapter biases
-    assert worst[0] < (2e-4 if precision == "fp32" else 0.2), worst
+    # L/14 (24 layers, fp32): the features carry ~1e-5 relative summation-order error, which
+    # the logit scale (100) turns into ~4e-4 on the adapter gradients: bound 1e-3 there
+    assert worst[0] < ((2e-4 if preset == "tiny" else 1e-3) if precision == "fp32" else 0.2), worst
 
 
 def test_trainer_three_steps_match_reference(golden, tmp_path):

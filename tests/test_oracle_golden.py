@@ -40,6 +40,7 @@ def batch(cfg, B, g):
     ("b32", "B/32", 8, True),
     ("b32_noadapter", "B/32", 8, False),
     ("b16", "B/16", 4, False),
+    ("l14", "L/14", 2, True),
 ])
 def test_forward_matches_reference(golden, tag, preset, B, adapters):
     g = golden(f"forward_{tag}.npz")

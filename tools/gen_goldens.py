@@ -134,6 +134,12 @@ def gen_forward(preset, B, tag, adapters=True, grads=False, layer=False, freeze_
     save(f"forward_{tag}.npz", **out)
 
 
+def gen_l14():
+    """Config 4's model: ViT-L/14 (P=14 -> patch K=588, N=257 tokens) + adapters, frozen towers, with the
+    adapter gradients (the trainable set of the adapter fine-tune)."""
+    gen_forward("L/14", 2, "l14", adapters=True, grads=True)
+
+
 def gen_contrastive():
     """The contrastive branch alone (model_m.py:146-171), fed synthetic features."""
     cfg = C.resolve("tiny")
@@ -251,3 +257,4 @@ if __name__ == "__main__":
     gen_forward("B/32", 8, "b32", adapters=True, layer=False)
     gen_forward("B/32", 8, "b32_noadapter", adapters=False)
     gen_forward("B/16", 4, "b16", adapters=False, layer=True)
+    gen_l14()

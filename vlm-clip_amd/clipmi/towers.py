@@ -239,9 +239,13 @@ class VisionTowerFn(torch.autograd.Function):
         dev = pixel_values.device
         px = pixel_values.contiguous() if raw else pixel_values.to(torch.float32).contiguous()
         N, D, Pp = v.num_positions, v.hidden_size, v.patch_size
-        Kp = v.num_channels * Pp * Pp
-        if Kp % 8:
-            raise NotImplementedError("patch K = 3*P*P must be a multiple of 8 (P=14 lands next round)")
+        Kc = v.num_channels * Pp * Pp
+        # patch K padded to a multiple of 64 (ViT-L/14: 588 -> 640) so both GEMM operands are
+        # 16-B aligned k-major rows the 256x256 LDS-DMA kernel takes; the pad columns are zero
+        # in the im2col rows and in the weight copy, so they add nothing
+        Kp = (Kc + 63) // 64 * 64 if Kc % 8 else Kc
+        if raw and Kp != Kc:
+            raise NotImplementedError("uint8 input step needs P % 8 == 0; pass normalised pixel_values for P=14")
         R = B * N
         train = rt.train_tower
         s = K.stream()
@@ -253,8 +257,10 @@ class VisionTowerFn(torch.autograd.Function):
         else:
             call("clipmi_im2col", s, dc, P_(px), P_(X), B, v.num_channels, H, Pp, Kp)
         h0 = torch.empty(R, D, dtype=dtype, device=dev)
-        K.gemm(R, D, Kp, X, Kp, True, arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kp),
-               Kp, True, h0, D)
+        Wp = arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kc)
+        if Kp != Kc:
+            Wp = torch.nn.functional.pad(Wp, (0, Kp - Kc))
+        K.gemm(R, D, Kp, X, Kp, True, Wp, Kp, True, h0, D)
         buf, acts = rt.venc.alloc(B, N, dtype, dev, train)
         stats0 = torch.empty(2, R, dtype=torch.float32, device=dev)
         call("clipmi_layernorm_fwd", s, dc, P_(h0), D, acts[0].x_in, D,
@@ -295,14 +301,18 @@ class VisionTowerFn(torch.autograd.Function):
              arena.ptr("vision_model.pre_layrnorm.weight", wbuf), P_(dh0), D, None, 0,
              arena.ptr("vision_model.pre_layrnorm.weight", g), arena.ptr("vision_model.pre_layrnorm.bias", g), 1,
              P_(lws), lws.numel(), R, D)
-        Kp = ctx.X.shape[1]
-        gW = arena.view("vision_model.embeddings.patch_embedding.weight", g).view(D, Kp)
+        Kp, Kc = ctx.X.shape[1], v.num_channels * v.patch_size ** 2
+        gW = arena.view("vision_model.embeddings.patch_embedding.weight", g).view(D, Kc)
+        if Kp != Kc:  # padded patch K: accumulate the [D, Kp] product's first Kc columns
+            gW_arena, gW = gW, torch.zeros(D, Kp, dtype=gW.dtype, device=dev)
         splits = max(1, min(32, 1024 // max(1, ((D + 127) // 128) * ((Kp + 127) // 128))))
         while splits > 1 and R // splits < 512:
             splits -= 1
         wsp = _ws(splits * D * Kp * 4, dev) if splits > 1 else None
         K.gemm(D, Kp, R, dh0, D, False, ctx.X, Kp, False, gW, Kp, flags=_lib.EPI_BETA, split_k=splits,
                workspace=wsp)
+        if Kp != Kc:
+            gW_arena.add_(gW[:, :Kc])
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
              arena.ptr("vision_model.embeddings.position_embedding.weight", g), 1)
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, 1, D, arena.ptr("vision_model.embeddings.class_embedding", g), 1)

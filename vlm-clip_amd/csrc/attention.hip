@@ -7,7 +7,8 @@
 // is written [B*N, D] so the out-projection GEMM consumes it directly.  The forward saves
 // the per-row log-sum-exp so the backward recomputes P without storing N x N scores.
 //
-// bf16 path (N <= 256): persistent workgroups walk (batch, head) items; the next item's
+// bf16 path (N <= 288, ATTN_MAX_N: two double-buffered K/V images of 288 rows fill the 160 KiB
+// LDS; covers ViT-B and ViT-L/14 at 224 px, N = 257): persistent workgroups walk (batch, head) items; the next item's
 // operands are LDS-DMA'd while the current one is computed (attn_fwd_pf, attn_bwd_pf).
 // K/V (and Q/dO/O in the backward) live in LDS as [Npad][64] bf16 images with 16-B chunk
 // c of row r stored at c ^ (r & 6); that single swizzle is conflict-free for the
@@ -27,6 +28,7 @@
 
 namespace {
 
+constexpr int ATTN_MAX_N = 288;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 constexpr float NEG_INF = -__builtin_huge_valf();
@@ -917,7 +919,8 @@ int fwd_dispatch(const AttnP& p, int causal, hipStream_t s) {
     case 12: launch_fwd_pf<12, M>(p, causal, s); return CLIPMI_OK;
     case 14: launch_fwd_pf<14, M>(p, causal, s); return CLIPMI_OK;
     case 16: launch_fwd_pf<16, M>(p, causal, s); return CLIPMI_OK;
-    default: return clipmi_invalid("attention: N must be <= 256");
+    case 18: launch_fwd_pf<18, M>(p, causal, s); return CLIPMI_OK;  // ViT-L/14 at 224: N = 257
+    default: return clipmi_invalid("attention: N must be <= 288");
   }
 }
 
@@ -953,7 +956,7 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
                                     const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
-  CLIPMI_REQUIRE(N >= 1 && N <= 256, "N must be in [1, 256]");
+  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N, "N must be in [1, 288]");
   if (B == 0) return CLIPMI_OK;
   const int npad = (N + 31) & ~31;
   // algorithmic FLOPs: QK^T and PV over the padded key range, B*H heads
@@ -982,7 +985,7 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
                                     int B, int H, int N, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
-  CLIPMI_REQUIRE(N >= 1 && N <= 256, "N must be in [1, 256]");
+  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N, "N must be in [1, 288]");
   if (B == 0) return CLIPMI_OK;
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
