@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
-    ap.add_argument("--roofline-kernel", default="gemm256_wgrad_splitk")
+    ap.add_argument("--roofline-kernel", default=None,
+                    help="kernel family timed live (default: gemm256_wgrad_splitk for --mode full, "
+                         "gemm256_fwd_bias_qgelu = the frozen vision tower's fc1 for --mode adapter)")
     ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     return ap.parse_args()
@@ -89,6 +91,15 @@ def wgrad_algorithmic_bytes(cfg, B):
     shapes.append((B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, 3 * v.patch_size ** 2))
     tot = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes)
     return round(tot / len(shapes))
+
+
+def fc1_algorithmic_bytes(cfg, B):
+    """Compulsory HBM bytes of one frozen-tower vision fc1 launch (gemm256_fwd_bias_qgelu, the
+    adapter-mode roofline kernel): LN'd activations [R, D] and weight [F, D] read once, the
+    activated [R, F] output written once, bf16, plus the bias."""
+    v = cfg.vision_config
+    R, D, F = B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, v.intermediate_size
+    return 2 * (R * D + F * D + R * F + F)
 
 
 def cpu_baseline(cfg, B, steps):
@@ -156,6 +167,8 @@ def main():
 
     cfg = C.resolve(args.model)
     adapters = args.mode == "adapter"
+    if args.roofline_kernel is None:
+        args.roofline_kernel = "gemm256_fwd_bias_qgelu" if adapters else "gemm256_wgrad_splitk"
     model = CLIPWithAdapters(args.model, use_text_adapter=adapters, use_vision_adapter=adapters,
                              use_shared_adapters=False, freeze_clip=adapters, device=dev, precision="bf16",
                              fast_init=True, process_group=group)
@@ -248,16 +261,18 @@ def main():
                 "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                "algorithmic_bytes": wgrad_algorithmic_bytes(cfg, args.batch)}
+                "algorithmic_bytes": (fc1_algorithmic_bytes(cfg, args.batch) if adapters
+                                      else wgrad_algorithmic_bytes(cfg, args.batch))}
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic: CLIP-normalised U[0,1) 224x224 pixels + BOS/random-id/EOS captions (77 tok, EOS pad), "
+        "data": f"synthetic: CLIP-normalised U[0,1) {cfg.vision_config.image_size}px pixels + BOS/random-id/EOS captions (77 tok, EOS pad), "
                 "random-init weights",
         "config": {"workload": f"{cfg.name} {'full fine-tune (adapters off)' if not adapters else 'adapter fine-tune'}"
                                f" contrastive step: fwd+bwd+all-reduce+clip+AdamW",
-                   "per_gpu_batch": args.batch, "global_batch": args.batch * world, "image_size": 224,
+                   "per_gpu_batch": args.batch, "global_batch": args.batch * world,
+                   "image_size": cfg.vision_config.image_size,
                    "text_len": 77, "parallelism": f"dp{world}"},
         "mfma_frac_step": round(value * step_flops_pair / (world * PEAK_BF16_TFLOPS * 1e12), 4),
         "step_tflops_per_gpu": round(value * step_flops_pair / world / 1e12, 1),

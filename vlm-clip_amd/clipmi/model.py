@@ -189,16 +189,28 @@ class CLIPWithAdapters(nn.Module):
         if self.use_shared_adapters:
             raise NotImplementedError("shared adapters (model_m.py:95-100) are not supported: the reference "
                                       "crashes for batch > 1 there (SURVEY quirk Q3)")
-        h = self.text_hidden_states(input_ids, attention_mask)
+        self._rt.train_tower = self._tower_training()
+        ids = self._check_device(input_ids)
+        mask = self._check_device(attention_mask) if attention_mask is not None else None
+        h = T.TextTowerFn.apply(ids, mask, _anchor(self.clip), self._rt)
         idx = None
         if self.pooling == "eos":
             t = self.config.text_config
-            ids = self._check_device(input_ids).to(torch.int64).contiguous()
+            ids = ids.to(torch.int64).contiguous()
             idx = torch.empty(ids.shape[0], dtype=torch.int32, device=ids.device)
             mode = 2 if t.eos_token_id == 2 else 1
             T.call("clipmi_pool_index", T.K.stream(), T.P_(ids), ids.shape[0], ids.shape[1], t.eos_token_id, mode,
                    T.P_(idx))
+        if self.use_text_adapter:
+            # the adapter is row-wise (down/GELU/up/residual/LN per token) and only the pooled
+            # row reaches the features (model_m.py:102), so it runs on that row alone: the same
+            # values as adapting all 77 tokens and then pooling, at 1/77 of the work
+            h = T.PoolRowsFn.apply(h, self._rt, idx)
+            h = T.AdapterFn.apply(h, _anchor(self.text_adapter), self._rt, self.text_adapter,
+                                  self._adapter_needs_grad(self.text_adapter, h))
+            idx = None
         return T.PoolProjFn.apply(h, self.clip.text_projection.weight, self._rt, "text_projection.weight", idx)
+
 
     def vision_hidden_states(self, pixel_values):
         self._rt.train_tower = self._tower_training()
@@ -211,7 +223,12 @@ class CLIPWithAdapters(nn.Module):
 
     def get_image_features(self, pixel_values):
         """model_m.py:107-125: vision tower (no post-LN, quirk Q2) -> adapter -> CLS -> visual_projection."""
-        h = self.vision_hidden_states(pixel_values)
+        self._rt.train_tower = self._tower_training()
+        h = T.VisionTowerFn.apply(self._check_device(pixel_values), _anchor(self.clip), self._rt)
+        if self.use_vision_adapter:  # CLS row only (model_m.py:122), as in get_text_features
+            h = T.PoolRowsFn.apply(h, self._rt, None)
+            h = T.AdapterFn.apply(h, _anchor(self.vision_adapter), self._rt, self.vision_adapter,
+                                  self._adapter_needs_grad(self.vision_adapter, h))
         return T.PoolProjFn.apply(h, self.clip.visual_projection.weight, self._rt, "visual_projection.weight", None)
 
     # ------------------------------------------------------------------ forward

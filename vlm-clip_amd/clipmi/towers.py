@@ -528,6 +528,31 @@ class PoolProjFn(torch.autograd.Function):
         return dh, None, None, None, None
 
 
+class PoolRowsFn(torch.autograd.Function):
+    """[B, S, D] -> [B, 1, D]: the pooled token of each sequence (idx None -> token 0), gathered
+    by clipmi_gather_rows; backward scatters the row gradients into zeros (clipmi_scatter_rows).
+    Lets the row-wise adapters run on the pooled rows only (model_m.py:102,122)."""
+
+    @staticmethod
+    def forward(ctx, h, runtime, idx):
+        dtype = runtime.dtype
+        B, S, D = h.shape
+        hc = h.to(dtype).contiguous()
+        out = torch.empty(B, 1, D, dtype=dtype, device=h.device)
+        call("clipmi_gather_rows", K.stream(), dcode(dtype), P_(hc), P_(idx), B, S, D, P_(out))
+        ctx.rt, ctx.idx, ctx.shape = runtime, idx, (B, S, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dtype = ctx.rt.dtype
+        B, S, D = ctx.shape
+        d = dout.to(dtype).contiguous()
+        dh = torch.zeros(B, S, D, dtype=dtype, device=dout.device)
+        call("clipmi_scatter_rows", K.stream(), dcode(dtype), P_(d), P_(ctx.idx), B, S, D, P_(dh), 0)
+        return dh, None, None
+
+
 # ------------------------------------------------------------------------------ contrastive
 def _rccl(group):
     return dist.get_backend(group) == "nccl"
