@@ -174,6 +174,34 @@ int clipmi_adamw(void* stream, float* p, const float* g, float* m, float* v, voi
                  double beta1, double beta2, double eps, double weight_decay, int step, const float* clip);
 int clipmi_cast_f32_bf16(void* stream, const float* src, void* dst, int64_t n);
 
+/* ---- Feature-level adapter heads (model_t.py CLIPAdapter / ZeroShot) -----
+ * All fp32, rows of E <= 1024 features, bottleneck A <= 256, C <= 1024 classes.
+ * clipmi_feature_adapter_fwd replaces VisualAdapter/TextAdapter.forward (model_t.py:13-33) fused
+ * with the residual blend and renormalisation of model_t.py:186-197 (visual, norm_in = 1: the
+ * input is normalised first, model_t.py:182-183) and :113-119 / :200-207 (text prototypes,
+ * norm_in = 0): xn = norm_in ? x/|x| : x; h = relu(W1 xn + b1); z = alpha (W2 h + b2) +
+ * (1 - alpha) xn; out = z/|z|; rz = 1/|z|.  W1 [A, E], W2 [E, A] (nn.Linear layout). */
+int clipmi_feature_adapter_fwd(void* stream, const float* x, int B, int E, int A, const float* W1, const float* b1,
+                               const float* W2, const float* b2, float alpha, int norm_in, float* xn, float* h,
+                               float* out, float* rz);
+int clipmi_feature_adapter_bwd_ws(int B, int E, int A);
+/* grads = [dW1 | db1 | dW2 | db2] (flat, fp32) += the batch's gradients given dout = dL/dout. */
+int clipmi_feature_adapter_bwd(void* stream, const float* dout, const float* out, const float* rz, const float* xn,
+                               const float* h, int B, int E, int A, const float* W2, float alpha, float* grads,
+                               void* workspace, int64_t workspace_bytes);
+/* Class scores (model_t.py:200-203 logits, :240-247 predict, :252-298 predict_with_all_descriptions):
+ * s[b, c] = max over descriptions j in [off[c], off[c+1]) of scale * img[b] . desc[j]; probs =
+ * softmax_c.  Any output may be NULL.  With labels (int64 [B]): loss_rows[b] = CE of row b,
+ * dscore = softmax - onehot, *bad = 1 on an out-of-range label. */
+int clipmi_class_scores(void* stream, const float* img, int B, int E, const float* desc, const int* off, int C,
+                        float scale, float* scores, float* probs, const int64_t* labels, float* loss_rows,
+                        float* dscore, int* bad);
+int clipmi_row_mean(void* stream, const float* v, int B, float* out);
+/* Mean-CE backward through prototype scores (one description per class): d = dscore * gscale[0] / B;
+ * dimg = scale d P, dprotos = scale d^T img.  gscale may be NULL (1). */
+int clipmi_class_ce_bwd(void* stream, const float* dscore, const float* img, const float* protos, int B, int C, int E,
+                        float scale, const float* gscale, float* dimg, float* dprotos);
+
 /* ---- Live kernel timing (bench.py roofline) --------------------------------------------------
  * While armed, every launch whose variant label equals `variant` (e.g. "gemm_fwd_bias_qgelu_pre",
  * "gemm_wgrad_splitk", "attn_fwd", "attn_bwd") is bracketed by hipEvents on its own stream,

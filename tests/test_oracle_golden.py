@@ -139,3 +139,29 @@ def test_image_processor_matches_hf(golden, tag):
     out = R.image_processor(g[f"{tag}_images"], 224, g["mean"], g["std"])
     assert out.shape == g[f"{tag}_pixel_values"].shape
     assert np.abs(out - g[f"{tag}_pixel_values"]).max() < 1e-5
+
+
+def test_heads_oracle_matches_reference(golden):
+    """oracle/heads_ref.py against model_t.CLIPAdapter / ZeroShotEmotionRecognition run from the reference."""
+    from oracle import heads_ref as H
+    from heads_common import fixture, weights, LN100
+    g = golden("heads.npz")
+    desc, img, labels = fixture()
+    assert digest(desc, img, labels) == str(g["input_digest"])
+    desc, img, labels = torch.from_numpy(desc), torch.from_numpy(img), torch.from_numpy(labels)
+    dn, protos = H.encode(desc, 5)
+    np.testing.assert_allclose(protos.numpy(), g["emotion_embedding_tensor"], atol=1e-6)
+    wv0, wt0 = weights(g, "init", "visual"), weights(g, "init", "text")
+    np.testing.assert_allclose(H.predict(img, protos, wv0, 0.2).numpy(), g["predict_untrained"], atol=1e-5)
+    batches = [torch.arange(i, i + 8) for i in range(0, 24, 8)]
+    temp = float(torch.tensor(LN100).exp())
+    wv, wt = H.train(img, protos, labels, wv0, wt0, 0.2, 0.2, temp, batches, 2, 3e-4)
+    for got, ref in zip(wv + wt, weights(g, "final", "visual") + weights(g, "final", "text")):
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), atol=2e-6)
+    adapted = H.blend(protos, wt, 0.2, False)
+    np.testing.assert_allclose(adapted.numpy(), g["adapted_emotion_embedding_tensor"], atol=1e-6)
+    np.testing.assert_allclose(H.predict(img, adapted, wv, 0.2).numpy(), g["predict"], atol=1e-5)
+    np.testing.assert_allclose(H.predict_all(img, dn, 5, wv, wt, 0.2, 0.2).numpy(), g["predict_all"], atol=1e-5)
+    zp, zpa = H.zero_shot(img, dn, protos, 5)
+    np.testing.assert_allclose(zp.numpy(), g["zs_predict"], atol=1e-5)
+    np.testing.assert_allclose(zpa.numpy(), g["zs_predict_all"], atol=1e-5)

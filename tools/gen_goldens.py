@@ -125,6 +125,8 @@ def gen_forward(preset, B, tag, adapters=True, grads=False, layer=False, freeze_
         out["text_eos_projected"] = ref.clip.text_projection(to.pooler_output).numpy()
         vo = ref.clip.vision_model(pixel_values=b["pixel_values"])
         out["vision_last_hidden_cls"] = vo.last_hidden_state.numpy()[:, 0]
+        # [HF] get_image_features semantics (CLS -> post_layernorm -> projection; model_t.py's backbone)
+        out["hf_image_features"] = ref.clip.visual_projection(vo.pooler_output).numpy()
         if layer:
             lay = ref.clip.vision_model.encoder.layers[0]
             x = torch.from_numpy(synth.normal((2, cfg.vision_config.num_positions, cfg.vision_config.hidden_size),
@@ -138,6 +140,80 @@ def gen_l14():
     """Config 4's model: ViT-L/14 (P=14 -> patch K=588, N=257 tokens) + adapters, frozen towers, with the
     adapter gradients (the trainable set of the adapter fine-tune)."""
     gen_forward("L/14", 2, "l14", adapters=True, grads=True)
+
+
+def heads_fixture():
+    """Feature tables + labels shared by the reference run below and the tests: 7 emotions x 5
+    descriptions of raw (unnormalised) text features, 24 images' raw features, E=512."""
+    E, n_desc, n_img = 512, 5, 24
+    desc = synth.normal((7 * n_desc, E), 7, "heads_desc")
+    img = synth.normal((n_img, E), 8, "heads_img")
+    labels = np.random.default_rng(9).integers(0, 7, n_img).astype(np.int64)
+    return desc, img, labels
+
+
+def gen_heads():
+    """model_t.CLIPAdapter (train 2 epochs x 3 batches of 8, predict, predict_with_all_descriptions)
+    and ZeroShotEmotionRecognition, run from the reference with the CLIP backbone replaced by a
+    feature lookup (the backbone's own features are pinned by the forward goldens) and the
+    processor by an index lookup (no tokenizer offline)."""
+    import model_t as MT
+    desc, img, labels = heads_fixture()
+    E, A = desc.shape[1], 64
+    emos = list(MT.EMOTIONS)
+    names = {f"{e}#{j}": i * 5 + j for i, e in enumerate(emos) for j in range(5)}
+
+    class Stub(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.logit_scale = torch.nn.Parameter(torch.tensor(float(np.log(100.0))))
+
+        def get_text_features(self, input_ids=None, **kw):
+            return torch.from_numpy(desc)[input_ids[:, 0]]
+
+        def get_image_features(self, pixel_values=None):
+            return torch.from_numpy(img)[pixel_values.long()]
+
+    class Inputs(dict):
+        def to(self, device):
+            return self
+
+    class Proc:
+        def __call__(self, text, **kw):
+            return Inputs(input_ids=torch.tensor([[names[text[0]]]]))
+
+    def setup(obj):
+        obj.model, obj.processor = Stub(), Proc()
+        obj.emotion_descriptions = {e: [f"{e}#{j}" for j in range(5)] for e in emos}
+        return obj
+
+    ca = setup(MT.CLIPAdapter.__new__(MT.CLIPAdapter))
+    torch.manual_seed(0)
+    ca.visual_adapter, ca.text_adapter = MT.VisualAdapter(E, A), MT.TextAdapter(E, A)
+    ca.alpha, ca.beta = 0.2, 0.2
+    out = {}
+    for nm, mod in (("visual", ca.visual_adapter), ("text", ca.text_adapter)):
+        for k, v in mod.state_dict().items():
+            out[f"init/{nm}/{k}"] = v.numpy().copy()
+    ca.encode_emotion_descriptions()
+    out["emotion_embedding_tensor"] = ca.emotion_embedding_tensor.numpy()
+    idx = torch.arange(img.shape[0])
+    loader = [(idx[i:i + 8], torch.from_numpy(labels[i:i + 8]), None) for i in range(0, 24, 8)]
+    with torch.no_grad():
+        out["predict_untrained"] = ca.predict(idx).numpy()
+    ca.train(loader, num_epochs=2, learning_rate=3e-4)
+    for nm, mod in (("visual", ca.visual_adapter), ("text", ca.text_adapter)):
+        for k, v in mod.state_dict().items():
+            out[f"final/{nm}/{k}"] = v.numpy().copy()
+    out["adapted_emotion_embedding_tensor"] = ca.adapted_emotion_embedding_tensor.numpy()
+    out["predict"] = ca.predict(idx).numpy()
+    out["predict_all"] = ca.predict_with_all_descriptions(idx).numpy()
+    zs = setup(MT.ZeroShotEmotionRecognition.__new__(MT.ZeroShotEmotionRecognition))
+    zs.encode_emotion_descriptions()
+    out["zs_predict"] = zs.predict(idx).numpy()
+    out["zs_predict_all"] = zs.predict_with_all_descriptions(idx).numpy()
+    out["input_digest"] = np.array(digest(desc, img, labels))
+    save("heads.npz", **out)
 
 
 def gen_contrastive():
@@ -258,3 +334,4 @@ if __name__ == "__main__":
     gen_forward("B/32", 8, "b32_noadapter", adapters=False)
     gen_forward("B/16", 4, "b16", adapters=False, layer=True)
     gen_l14()
+    gen_heads()
