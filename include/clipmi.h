@@ -202,6 +202,11 @@ int clipmi_row_mean(void* stream, const float* v, int B, float* out);
 int clipmi_class_ce_bwd(void* stream, const float* dscore, const float* img, const float* protos, int B, int C, int E,
                         float scale, const float* gscale, float* dimg, float* dprotos);
 
+/* Row softmax of scale*x (fp32, y may alias x) and its backward dx = scale*y*(dy - <dy, y>):
+ * the shared cross-attention adapter's probabilities (adapter/clip_adapter.py:117). */
+int clipmi_softmax_rows(void* stream, const float* x, float* y, int R, int N, float scale);
+int clipmi_softmax_rows_bwd(void* stream, const float* y, const float* dy, float* dx, int R, int N, float scale);
+
 /* ---- Live kernel timing (bench.py roofline) --------------------------------------------------
  * While armed, every launch whose variant label equals `variant` (e.g. "gemm_fwd_bias_qgelu_pre",
  * "gemm_wgrad_splitk", "attn_fwd", "attn_bwd") is bracketed by hipEvents on its own stream,

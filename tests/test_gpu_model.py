@@ -157,3 +157,39 @@ def test_uint8_images_match_processor_path(precision):
     torch.cuda.synchronize()
     tol = 1e-5 if precision == "fp32" else 2e-2
     assert (a["logits_per_text"] - u["logits_per_text"]).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_shared_adapters_match_reference(golden, precision):
+    """SharedMHSAttentionAdapter x2 (adapter/clip_adapter.py:69-128, model_m.py:95-100) with the
+    batch broadcast: features and gradients vs the reference run caption by caption (it only
+    runs at batch 1, quirk Q3), eval mode."""
+    g = golden("shared_adapters.npz")
+    m = CLIPWithAdapters("B/32", use_shared_adapters=True, freeze_clip=True, device="cuda", precision=precision)
+    b = batch(m.config, 4, g)
+    tf = m.get_text_features(b["input_ids"], b["attention_mask"])
+    ref = g["text_features_raw"]
+    err = float(np.abs(tf.detach().cpu().numpy() - ref).max() / np.abs(ref).max())
+    G = torch.from_numpy(synth.normal((4, m.config.projection_dim), 11, "shared_G")).cuda()
+    (tf * G).sum().backward()
+    torch.cuda.synchronize()
+    params = dict(m.named_parameters())
+    worst = (0.0, "")
+    for k in g.files:
+        if not k.startswith("grad/"):
+            continue
+        n = k[5:]
+        r = g[k]
+        got = params[n].grad
+        assert got is not None, n
+        got = got.cpu().numpy()
+        got = got if got.ndim == 1 else got[:8]
+        worst = max(worst, (float(np.abs(got - r).max() / max(np.abs(r).max(), 1e-8)), n))
+    print(f"\n[shared {precision}] features rel err {err:.3e}; worst grad rel err {worst[0]:.3e} at {worst[1]}")
+    assert err < (1e-4 if precision == "fp32" else 5e-2)
+    assert worst[0] < (1e-3 if precision == "fp32" else 0.2), worst
+    sd_path = "/tmp/clipmi_shared_ckpt.pt"
+    m.save_adapter_weights(sd_path)
+    sd = torch.load(sd_path, weights_only=True)
+    assert "shared_adapters" in sd and "0.cross_attn.in_proj_weight" in sd["shared_adapters"]
+    m.load_adapter_weights(sd_path)

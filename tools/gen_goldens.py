@@ -216,6 +216,40 @@ def gen_heads():
     save("heads.npz", **out)
 
 
+def gen_shared():
+    """model_m.CLIPWithAdapters with use_shared_adapters=True (B/32, 2 SharedMHSAttentionAdapter
+    layers, eval mode).  The reference only runs at batch 1 (quirk Q3), so each caption runs
+    alone: text features [4, E], and the gradients of L = sum_b <features_b, G_b> accumulated
+    over the four runs (= the batch-broadcast semantics) for the small tensors and the first 8
+    rows of each weight matrix."""
+    cfg = C.resolve("B/32")
+    import model_m
+    from transformers import CLIPConfig, CLIPModel
+    ref = build_reference_model(cfg, True, True, freeze_clip=True)
+    t, v = cfg.text_config, cfg.vision_config
+    ref.use_shared_adapters = True
+    ref.shared_adapters = torch.nn.ModuleList([model_m.SharedMHSAttentionAdapter(t.hidden_size, v.hidden_size)
+                                               for _ in range(2)])
+    for i, sa in enumerate(ref.shared_adapters):
+        sa.load_state_dict({k: torch.from_numpy(x) for k, x in synth.shared_adapter_state_dict(
+            t.hidden_size, v.hidden_size, 0, f"shared_adapters.{i}").items()})
+    ref.eval()
+    b_np, b = batch_tensors(cfg, 4)
+    G = torch.from_numpy(synth.normal((4, cfg.projection_dim), 11, "shared_G"))
+    feats = []
+    for i in range(4):
+        f = ref.get_text_features(b["input_ids"][i:i + 1], b["attention_mask"][i:i + 1])
+        (f * G[i:i + 1]).sum().backward()
+        feats.append(f.detach())
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"])),
+           "text_features_raw": torch.cat(feats).numpy()}
+    for k, p in ref.named_parameters():
+        if "shared_adapters" in k or "text_adapter" in k:
+            g = p.grad.numpy()
+            out[f"grad/{k}"] = g if g.ndim == 1 else g[:8]
+    save("shared_adapters.npz", **out)
+
+
 def gen_contrastive():
     """The contrastive branch alone (model_m.py:146-171), fed synthetic features."""
     cfg = C.resolve("tiny")
@@ -335,3 +369,4 @@ if __name__ == "__main__":
     gen_forward("B/16", 4, "b16", adapters=False, layer=True)
     gen_l14()
     gen_heads()
+    gen_shared()

@@ -110,9 +110,12 @@ class CLIPWithAdapters(nn.Module):
             self.vision_adapter.load_numpy(synth.adapter_state_dict(vision_hidden, vision_adapter_size, init_seed,
                                                                     "vision_adapter"))
         if use_shared_adapters:
-            warnings.warn("use_shared_adapters=True: the reference's SharedMHSAttentionAdapter path crashes for "
-                          "batch > 1 (model_m.py:96-98, SURVEY quirk Q3) and is not on the accelerated path yet; "
-                          "forward() will raise. Pass use_shared_adapters=False.", stacklevel=2)
+            # model_m.py:54-61: SharedMHSAttentionAdapter(text_hidden, vision_hidden) x layers;
+            # hidden 512, so text_projection only fits text_hidden == 512 (B/* models), as in the reference
+            from .shared_adapter import SharedAdapterParams
+            self.shared_adapters = nn.ModuleList([SharedAdapterParams(text_hidden, vision_hidden, device,
+                                                                      seed=init_seed, prefix=f"shared_adapters.{i}")
+                                                  for i in range(shared_adapter_layers)])
         self._rt = _Runtime(self.clip, dtype)
         if freeze_clip:
             self._freeze_clip_parameters()
@@ -160,6 +163,8 @@ class CLIPWithAdapters(nn.Module):
         for a in (self.text_adapter, self.vision_adapter):
             if a is not None:
                 out.append(a.arena)
+        for a in (self.shared_adapters or []):
+            out.append(a.arena)
         return out
 
     # ------------------------------------------------------------------ features
@@ -186,9 +191,6 @@ class CLIPWithAdapters(nn.Module):
 
     def get_text_features(self, input_ids, attention_mask):
         """model_m.py:77-105: text tower -> adapter -> token 0 -> text_projection."""
-        if self.use_shared_adapters:
-            raise NotImplementedError("shared adapters (model_m.py:95-100) are not supported: the reference "
-                                      "crashes for batch > 1 there (SURVEY quirk Q3)")
         self._rt.train_tower = self._tower_training()
         ids = self._check_device(input_ids)
         mask = self._check_device(attention_mask) if attention_mask is not None else None
@@ -201,14 +203,21 @@ class CLIPWithAdapters(nn.Module):
             mode = 2 if t.eos_token_id == 2 else 1
             T.call("clipmi_pool_index", T.K.stream(), T.P_(ids), ids.shape[0], ids.shape[1], t.eos_token_id, mode,
                    T.P_(idx))
+        if self.use_text_adapter or self.use_shared_adapters:
+            h = T.PoolRowsFn.apply(h, self._rt, idx)
+            idx = None
         if self.use_text_adapter:
             # the adapter is row-wise (down/GELU/up/residual/LN per token) and only the pooled
             # row reaches the features (model_m.py:102), so it runs on that row alone: the same
             # values as adapting all 77 tokens and then pooling, at 1/77 of the work
-            h = T.PoolRowsFn.apply(h, self._rt, idx)
             h = T.AdapterFn.apply(h, _anchor(self.text_adapter), self._rt, self.text_adapter,
                                   self._adapter_needs_grad(self.text_adapter, h))
-            idx = None
+        if self.use_shared_adapters:
+            # model_m.py:95-100: image tokens = the vision position embedding, shared by the batch
+            from .shared_adapter import SharedAdapterFn
+            pos = self.clip.arena.view("vision_model.embeddings.position_embedding.weight")
+            for sa in self.shared_adapters:
+                h = SharedAdapterFn.apply(h, _anchor(sa), sa, pos, self._adapter_needs_grad(sa, h))
         return T.PoolProjFn.apply(h, self.clip.text_projection.weight, self._rt, "text_projection.weight", idx)
 
 
@@ -301,7 +310,8 @@ class CLIPWithAdapters(nn.Module):
             adapter_state_dict["vision_adapter"] = {k: v.detach().clone()
                                                     for k, v in self.vision_adapter.state_dict().items()}
         if self.use_shared_adapters:
-            raise NotImplementedError("shared adapters are not supported (SURVEY quirk Q3)")
+            adapter_state_dict["shared_adapters"] = {k: v.detach().clone()
+                                                     for k, v in self.shared_adapters.state_dict().items()}
         if not adapter_state_dict:
             raise ValueError("No adapters enabled to save")
         d = os.path.dirname(save_path)
@@ -331,7 +341,7 @@ class CLIPWithAdapters(nn.Module):
         if "shared_adapters" in adapter_state_dict:
             if not self.use_shared_adapters:
                 raise ValueError("Shared adapter weights found but shared adapters are not enabled")
-            raise NotImplementedError("shared adapters are not supported (SURVEY quirk Q3)")
+            self.shared_adapters.load_state_dict(adapter_state_dict["shared_adapters"])
         elif self.use_shared_adapters:
             raise ValueError("Shared adapters are enabled but no weights found in checkpoint")
         print(f"Adapter weights loaded from {load_path}")

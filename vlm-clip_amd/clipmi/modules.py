@@ -69,7 +69,7 @@ def _attach(root: nn.Module, name: str, param: nn.Parameter):
         nxt_is_idx = parts[i + 1].isdigit()
         if isinstance(mod, nn.ModuleList):
             idx = int(part)
-            if idx == len(mod):
+            while idx >= len(mod):  # parameter-free slots (e.g. nn.Sequential's GELU at mlp.1) stay empty
                 mod.append(nn.ModuleList() if nxt_is_idx else nn.Module())
             mod = mod[idx]
         else:

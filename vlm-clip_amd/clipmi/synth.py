@@ -143,6 +143,29 @@ def adapter_state_dict(hidden: int, bottleneck: int, seed: int, prefix: str, ln:
     return sd
 
 
+def shared_adapter_state_dict(text_in: int, image_in: int, seed: int, prefix: str, hidden: int = 512):
+    """SharedMHSAttentionAdapter (adapter/clip_adapter.py:69-128) weights: linear weights
+    N(0, 1/fan_in), LayerNorm weights 1 + N(0, 0.1), biases N(0, 0.02)."""
+    H = hidden
+    shapes = [("text_proj.weight", (H, text_in)), ("text_proj.bias", (H,)),
+              ("image_proj.weight", (H, image_in)), ("image_proj.bias", (H,)),
+              ("cross_attn.in_proj_weight", (3 * H, H)), ("cross_attn.in_proj_bias", (3 * H,)),
+              ("cross_attn.out_proj.weight", (H, H)), ("cross_attn.out_proj.bias", (H,)),
+              ("norm1.weight", (H,)), ("norm1.bias", (H,)), ("norm2.weight", (H,)), ("norm2.bias", (H,)),
+              ("norm3.weight", (H,)), ("norm3.bias", (H,)),
+              ("mlp.0.weight", (4 * H, H)), ("mlp.0.bias", (4 * H,)),
+              ("mlp.2.weight", (H, 4 * H)), ("mlp.2.bias", (H,))]
+    sd = OrderedDict()
+    for name, shape in shapes:
+        if len(shape) == 2:
+            sd[name] = normal(shape, seed, f"{prefix}.{name}", 1.0 / math.sqrt(shape[1]))
+        elif name.startswith("norm") and name.endswith("weight"):
+            sd[name] = normal(shape, seed, f"{prefix}.{name}", 0.1, 1.0)
+        else:
+            sd[name] = normal(shape, seed, f"{prefix}.{name}", 0.02)
+    return sd
+
+
 CLIP_MEAN = np.array([0.48145466, 0.4578275, 0.40821073], dtype=np.float64)
 CLIP_STD = np.array([0.26862954, 0.26130258, 0.27577711], dtype=np.float64)
 

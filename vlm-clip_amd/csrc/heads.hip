@@ -216,7 +216,54 @@ __global__ __launch_bounds__(HT) void class_ce_bwd_kernel(const float* dscore, c
   }
 }
 
+// row softmax of scale * x (fp32, one wave per row; in place allowed): the cross-attention
+// probabilities of the shared adapter (nn.MultiheadAttention core, adapter/clip_adapter.py:117)
+__global__ __launch_bounds__(HT) void softmax_rows_kernel(const float* x, float* y, int R, int N, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (HT / 64) + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const float* xr = x + row * N;
+  float m = -__builtin_huge_valf();
+  for (int j = lane; j < N; j += 64) m = fmaxf(m, scale * xr[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < N; j += 64) s += expf(scale * xr[j] - m);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int j = lane; j < N; j += 64) y[row * N + j] = expf(scale * xr[j] - m) * inv;
+}
+
+// dx = scale * y * (dy - sum_j dy_j y_j)
+__global__ __launch_bounds__(HT) void softmax_rows_bwd_kernel(const float* y, const float* dy, float* dx, int R, int N,
+                                                             float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (HT / 64) + (threadIdx.x >> 6);
+  if (row >= R) return;
+  float d = 0.f;
+  for (int j = lane; j < N; j += 64) d += dy[row * N + j] * y[row * N + j];
+  d = wave_sum(d);
+  for (int j = lane; j < N; j += 64) dx[row * N + j] = scale * y[row * N + j] * (dy[row * N + j] - d);
+}
+
 }  // namespace
+
+extern "C" int clipmi_softmax_rows(void* stream, const float* x, float* y, int R, int N, float scale) {
+  CLIPMI_REQUIRE(R >= 0 && N >= 1, "softmax: bad shape");
+  if (R == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((R + 3) / 4), dim3(HT), 0, (hipStream_t)stream, x, y, R, N, scale);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_softmax_rows_bwd(void* stream, const float* y, const float* dy, float* dx, int R, int N,
+                                       float scale) {
+  CLIPMI_REQUIRE(R >= 0 && N >= 1, "softmax: bad shape");
+  if (R == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(softmax_rows_bwd_kernel, dim3((R + 3) / 4), dim3(HT), 0, (hipStream_t)stream, y, dy, dx, R, N,
+                     scale);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
 
 extern "C" int clipmi_feature_adapter_fwd(void* stream, const float* x, int B, int E, int A, const float* W1,
                                           const float* b1, const float* W2, const float* b2, float alpha, int norm_in,
