@@ -148,14 +148,42 @@ def adapter(x, a, layer_norm_on=True, eps=1e-5):
     return h
 
 
-def text_features(input_ids, attention_mask, p, cfg, text_adapter=None, pooling="first"):
+def shared_adapter(x, img, s, heads=8):
+    """SharedMHSAttentionAdapter.forward, adapter/clip_adapter.py:100-128 (eval mode), with the
+    image tokens img [N_v, D_v] broadcast over the batch (quirk Q3; the reference runs at B=1).
+    nn.MultiheadAttention core restated: q,k,v = in_proj; softmax(q k^T / sqrt(64)) v; out_proj."""
+    t = linear(x, s["text_proj.weight"], s["text_proj.bias"])
+    u = linear(img, s["image_proj.weight"], s["image_proj.bias"])
+    kv = layer_norm(u, s["norm1.weight"], s["norm1.bias"], 1e-5)
+    hs = layer_norm(t, s["norm2.weight"], s["norm2.bias"], 1e-5)
+    W, b = s["cross_attn.in_proj_weight"], s["cross_attn.in_proj_bias"]
+    H = W.shape[1]
+    q = linear(hs, W[:H], b[:H])
+    k = linear(kv, W[H:2 * H], b[H:2 * H])
+    v = linear(kv, W[2 * H:], b[2 * H:])
+    B, T = q.shape[0], q.shape[1]
+    hd = H // heads
+    qh = q.view(B, T, heads, hd).transpose(1, 2)
+    kh = k.view(-1, heads, hd).transpose(0, 1)
+    vh = v.view(-1, heads, hd).transpose(0, 1)
+    a = torch.softmax((qh @ kh.transpose(-1, -2)) * hd ** -0.5, dim=-1) @ vh
+    a = a.transpose(1, 2).reshape(B, T, H)
+    hs = hs + linear(a, s["cross_attn.out_proj.weight"], s["cross_attn.out_proj.bias"])
+    m = gelu_erf(linear(layer_norm(hs, s["norm3.weight"], s["norm3.bias"], 1e-5), s["mlp.0.weight"], s["mlp.0.bias"]))
+    return hs + linear(m, s["mlp.2.weight"], s["mlp.2.bias"])
+
+
+def text_features(input_ids, attention_mask, p, cfg, text_adapter=None, pooling="first", shared_adapters=None):
     """CLIPWithAdapters.get_text_features, model_m.py:77-105.
 
     pooling="first" reproduces ``text_features[:, 0, :]`` (model_m.py:102, quirk Q1);
-    pooling="eos" is HF CLIPTextModel's pooler ([HF] :561-581)."""
+    pooling="eos" is HF CLIPTextModel's pooler ([HF] :561-581).  shared_adapters: list of
+    SharedMHSAttentionAdapter state dicts applied after the text adapter (model_m.py:95-100)."""
     h = text_tower(input_ids, attention_mask, p, cfg)
     if text_adapter is not None:
         h = adapter(h, text_adapter)                                          # :88-90
+    for s in shared_adapters or []:
+        h = shared_adapter(h, p["vision_model.embeddings.position_embedding.weight"], s)  # :95-100
     if pooling == "first":
         pooled = h[:, 0, :]
     else:

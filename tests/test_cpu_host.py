@@ -208,3 +208,23 @@ def test_data_parallel_contrastive_decomposition_gloo():
         assert abs(lsum - ref.item()) < 1e-12
         np.testing.assert_allclose(gt, tg.grad[rank * 4:(rank + 1) * 4].numpy(), atol=1e-12)
         np.testing.assert_allclose(gi, ig.grad[rank * 4:(rank + 1) * 4].numpy(), atol=1e-12)
+
+
+def test_shared_adapter_state_dict_schema():
+    """shared_adapters.* names/shapes equal SharedMHSAttentionAdapter's (adapter/clip_adapter.py:70-97:
+    Linear text/image projections, nn.MultiheadAttention, 3 LayerNorms, Sequential MLP)."""
+    import torch.nn as nn
+    from clipmi import CLIPWithAdapters
+    m = CLIPWithAdapters("tiny", use_shared_adapters=True, shared_adapter_layers=2, device="cpu")
+    t, v = m.config.text_config.hidden_size, m.config.vision_config.hidden_size
+    H = 512
+    ref = nn.ModuleDict(dict(text_proj=nn.Linear(t, H), image_proj=nn.Linear(v, H),
+                             cross_attn=nn.MultiheadAttention(H, 8, batch_first=True),
+                             norm1=nn.LayerNorm(H), norm2=nn.LayerNorm(H), norm3=nn.LayerNorm(H),
+                             mlp=nn.Sequential(nn.Linear(H, 4 * H), nn.GELU(), nn.Linear(4 * H, H), nn.Dropout(0.1))))
+    want = {k: tuple(x.shape) for k, x in ref.state_dict().items()}
+    got = {k: tuple(x.shape) for k, x in m.shared_adapters[1].state_dict().items()}
+    assert got == want
+    names = [n for n, _ in m.named_parameters() if "shared_adapters" in n]
+    assert len(names) == 2 * len(want) and all("adapter" in n for n in names)
+    assert len(m.arenas()) == 5

@@ -165,3 +165,17 @@ def test_heads_oracle_matches_reference(golden):
     zp, zpa = H.zero_shot(img, dn, protos, 5)
     np.testing.assert_allclose(zp.numpy(), g["zs_predict"], atol=1e-5)
     np.testing.assert_allclose(zpa.numpy(), g["zs_predict_all"], atol=1e-5)
+
+
+def test_shared_adapters_oracle_matches_reference(golden):
+    """oracle shared_adapter (batch broadcast) against the reference run caption by caption."""
+    g = golden("shared_adapters.npz")
+    cfg = C.resolve("B/32")
+    p, ta, _ = model_params(cfg, True)
+    t, v = cfg.text_config, cfg.vision_config
+    sh = [R.to_torch(synth.shared_adapter_state_dict(t.hidden_size, v.hidden_size, 0, f"shared_adapters.{i}"))
+          for i in range(2)]
+    b = batch(cfg, 4, g)
+    with torch.no_grad():
+        f = R.text_features(b["input_ids"], b["attention_mask"], p, cfg, ta, shared_adapters=sh)
+    np.testing.assert_allclose(f.numpy(), g["text_features_raw"], atol=2e-5, rtol=1e-4)
