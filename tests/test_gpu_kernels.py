@@ -254,14 +254,16 @@ def test_adamw_and_clip_match_torch():
 
 @pytest.mark.parametrize("tag", ["sq", "crop"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_im2col_uint8_matches_processor(golden, tag, dtype):
+@pytest.mark.parametrize("P", [16, 14])
+def test_im2col_uint8_matches_processor(golden, tag, dtype, P):
     """Fused input step (uint8 NHWC -> crop + rescale + normalise + im2col) vs im2col of the
     reference processor's pixel_values (tests/golden/image_processor.npz)."""
     g = golden("image_processor.npz")
     imgs = torch.from_numpy(g[f"{tag}_images"]).cuda()
     pv = torch.from_numpy(g[f"{tag}_pixel_values"]).cuda()
-    B, P, S = imgs.shape[0], 16, 224
-    Kp = 3 * P * P
+    B, S = imgs.shape[0], 224
+    Kc = 3 * P * P
+    Kp = (Kc + 63) // 64 * 64 if Kc % 8 else Kc  # P=14 (ViT-L/14): 588 padded to 640, pad columns zeroed
     R = B * ((S // P) ** 2 + 1)
     X = torch.full((R, Kp), 7.0, device="cuda", dtype=dtype)
     T.im2col_uint8(imgs, X, S, P)

@@ -244,8 +244,6 @@ class VisionTowerFn(torch.autograd.Function):
         # 16-B aligned k-major rows the 256x256 LDS-DMA kernel takes; the pad columns are zero
         # in the im2col rows and in the weight copy, so they add nothing
         Kp = (Kc + 63) // 64 * 64 if Kc % 8 else Kc
-        if raw and Kp != Kc:
-            raise NotImplementedError("uint8 input step needs P % 8 == 0; pass normalised pixel_values for P=14")
         R = B * N
         train = rt.train_tower
         s = K.stream()

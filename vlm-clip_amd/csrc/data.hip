@@ -60,41 +60,49 @@ __global__ __launch_bounds__(256) void im2col8_kernel(const float* px, T* X, int
 // last (what CLIPImageProcessor receives), centre-cropped to G*P, rescaled by 1/255 and
 // normalised per channel ([HF] image_processing_clip.py: center_crop, rescale, normalize;
 // do_resize stays on the host), written straight as im2col rows.  One thread per (token, ky,
-// 8 consecutive kx): a 24-B read of 8 RGB pixels, three 8-element writes (one per channel).
-template <typename T>
+// GW consecutive kx): GW = 8 for P % 8 == 0 (a 24-B read of 8 RGB pixels, three 8-element
+// writes, one per channel), GW = 2 for ViT-L/14 (P = 14, whose padded K columns it zeroes).
+template <typename T, int GW>
 __global__ __launch_bounds__(256) void im2col_u8_kernel(const uint8_t* img, T* X, int64_t rows, int Hin, int Win,
                                                         int y0, int x0, int P, int G, int Kp, float m0, float m1,
                                                         float m2, float r0, float r1, float r2) {
-  const int per_row = P * (P / 8);  // (ky, kx-group) pairs per token
+  const int per_row = P * (P / GW);  // (ky, kx-group) pairs per token
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t row = id / per_row;
   if (row >= rows) return;
   const int q = (int)(id - row * per_row);
-  const int ky = q / (P / 8), kx = (q - ky * (P / 8)) * 8;
+  const int ky = q / (P / GW), kx = (q - ky * (P / GW)) * GW;
   const int Np1 = G * G + 1;
   const int b = (int)(row / Np1), t = (int)(row - (int64_t)b * Np1);
-  float v[3][8];
+  float v[3][GW];
   if (t == 0) {  // CLS slot: zero row (the class embedding is added after the patch GEMM)
 #pragma unroll
     for (int c = 0; c < 3; ++c)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      for (int j = 0; j < GW; ++j) v[c][j] = 0.f;
   } else {
     const int p = t - 1, gy = p / G, gx = p - gy * G;
     const int y = y0 + gy * P + ky, x = x0 + gx * P + kx;
     const uint8_t* src = img + (((int64_t)b * Hin + y) * Win + x) * 3;
     const float mean[3] = {m0, m1, m2}, rstd[3] = {r0, r1, r2};
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < GW; ++j)
 #pragma unroll
       for (int c = 0; c < 3; ++c) v[c][j] = ((float)src[3 * j + c] * (1.0f / 255.0f) - mean[c]) * rstd[c];
   }
   T* dst = X + row * Kp + ky * P + kx;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    store4(dst + c * P * P, v[c]);
-    store4(dst + c * P * P + 4, v[c] + 4);
+    if constexpr (GW == 8) {
+      store4(dst + c * P * P, v[c]);
+      store4(dst + c * P * P + 4, v[c] + 4);
+    } else {
+#pragma unroll
+      for (int j = 0; j < GW; ++j) dst[c * P * P + j] = (T)v[c][j];
+    }
   }
+  if (q == 0)  // padded K (ViT-L/14: 588 -> 640): zero the pad columns once per token row
+    for (int k = 3 * P * P; k < Kp; ++k) X[row * Kp + k] = (T)0.f;
 }
 
 // idx[b] = pooled token: mode 0 -> 0, mode 1 -> first position with id == eos, mode 2 -> argmax id
@@ -160,23 +168,27 @@ extern "C" int clipmi_im2col(void* stream, int dtype, const float* pixels, void*
 
 extern "C" int clipmi_im2col_u8(void* stream, int dtype, const uint8_t* images, void* X, int B, int Hin, int Win,
                                 int image_size, int P, int Kp, const float* mean, const float* std) {
-  CLIPMI_REQUIRE(image_size % P == 0 && P % 8 == 0, "image size must be a multiple of the patch size, P % 8 == 0");
+  CLIPMI_REQUIRE(image_size % P == 0 && P % 2 == 0, "image size must be a multiple of the patch size, P even");
   CLIPMI_REQUIRE(Hin >= image_size && Win >= image_size, "images smaller than the crop (resize them first)");
-  CLIPMI_REQUIRE(Kp == 3 * P * P, "Kp must be 3*P*P");
+  CLIPMI_REQUIRE(Kp >= 3 * P * P && (Kp == 3 * P * P || Kp % 8 == 0), "Kp must be 3*P*P or a padded multiple of 8");
   CLIPMI_REQUIRE(mean && std && std[0] != 0.f && std[1] != 0.f && std[2] != 0.f, "mean/std");
   const int G = image_size / P;
   const int64_t rows = (int64_t)B * (G * G + 1);
   if (rows == 0) return CLIPMI_OK;
   const int y0 = (Hin - image_size) / 2, x0 = (Win - image_size) / 2;  // [HF] center_crop offsets
-  const int64_t n = rows * P * (P / 8);
+  const int gw = P % 8 == 0 ? 8 : 2;  // 8 pixels (24 B) per thread for P = 16/32, 2 for P = 14
+  const int64_t n = rows * P * (P / gw);
   const unsigned nb = (unsigned)((n + 255) / 256);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == CLIPMI_BF16)
-    hipLaunchKernelGGL(im2col_u8_kernel<bf16>, dim3(nb), dim3(256), 0, s, images, (bf16*)X, rows, Hin, Win, y0, x0, P, G,
-                       Kp, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2]);
-  else
-    hipLaunchKernelGGL(im2col_u8_kernel<float>, dim3(nb), dim3(256), 0, s, images, (float*)X, rows, Hin, Win, y0, x0, P,
-                       G, Kp, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2]);
+  const float r0 = 1.f / std[0], r1 = 1.f / std[1], r2 = 1.f / std[2];
+#define CLIPMI_U8(T, GW) hipLaunchKernelGGL((im2col_u8_kernel<T, GW>), dim3(nb), dim3(256), 0, s, images, (T*)X, rows, \
+                                            Hin, Win, y0, x0, P, G, Kp, mean[0], mean[1], mean[2], r0, r1, r2)
+  if (dtype == CLIPMI_BF16) {
+    if (gw == 8) CLIPMI_U8(bf16, 8); else CLIPMI_U8(bf16, 2);
+  } else {
+    if (gw == 8) CLIPMI_U8(float, 8); else CLIPMI_U8(float, 2);
+  }
+#undef CLIPMI_U8
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
