@@ -53,11 +53,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
-    ap.add_argument("--roofline-kernel", default=None,
-                    help="kernel family timed live (default: gemm256_wgrad_splitk for --mode full, "
-                         "gemm256_fwd_bias_qgelu = the frozen vision tower's fc1 for --mode adapter)")
+    ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES),
+                    help="family reported as `roofline` (default: the one with the most measured time)")
     ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: each rank prints its rank/world and exits before touching the GPU")
     return ap.parse_args()
 
 
@@ -78,28 +79,47 @@ def synthetic_batch(cfg, B, rank, device, seed=1234):
     return {"input_ids": ids, "attention_mask": mask, "pixel_values": px.contiguous()}
 
 
-def wgrad_algorithmic_bytes(cfg, B):
-    """Mean compulsory HBM bytes of one gemm256_wgrad_splitk launch the live roofline times:
-    both bf16 operands read once (tokens x (M + N) x 2 B) + the fp32 gradient written once
-    (M x N x 4 B), over the vision tower's 49 wgrad launches per step (4 per encoder layer +
-    the patch embedding; the text tower's run on the second stream and are not timed)."""
-    v = cfg.vision_config
-    shapes = []
-    for tc, R in ((v, B * ((v.image_size // v.patch_size) ** 2 + 1)),):
-        D, F = tc.hidden_size, tc.intermediate_size
-        shapes += [(R, D, F), (R, F, D), (R, D, D), (R, 3 * D, D)] * tc.num_hidden_layers
-    shapes.append((B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, 3 * v.patch_size ** 2))
-    tot = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes)
-    return round(tot / len(shapes))
+# Kernel families timed live (labels returned by libclipmi's dispatch, csrc/gemm.hip, attention.hip)
+FAMILIES = {
+    "gemm256_fwd_dgrad": ["gemm256_fwd_bias", "gemm256_fwd_bias_resid", "gemm256_fwd_bias_qgelu_pre",
+                          "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad", "gemm256_dgrad_dqgelu"],
+    "gemm256_wgrad": ["gemm256_wgrad_splitk", "gemm256_wgrad"],
+    "attention": ["attn_fwd", "attn_bwd"],
+}
+# HBM traffic per launch of each family, from rocprofv3 --pmc passes (tools/traffic_pmc.sh); named
+# explicitly so the file read is the one committed for this build, not the newest on disk
+TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r02_traffic_fwd_dgrad.json",
+                 "gemm256_wgrad": "profiles/r02_traffic_wgrad.json"}
 
 
-def fc1_algorithmic_bytes(cfg, B):
-    """Compulsory HBM bytes of one frozen-tower vision fc1 launch (gemm256_fwd_bias_qgelu, the
-    adapter-mode roofline kernel): LN'd activations [R, D] and weight [F, D] read once, the
-    activated [R, F] output written once, bf16, plus the bias."""
+def vision_gemm_shapes(cfg, B, train):
+    """(M, N, K, extra_bytes) of the vision tower's 256-kernel launches on the caller's stream,
+    per step, in the families above; extra = epilogue operands/outputs beyond A, B and C once."""
     v = cfg.vision_config
-    R, D, F = B * ((v.image_size // v.patch_size) ** 2 + 1), v.hidden_size, v.intermediate_size
-    return 2 * (R * D + F * D + R * F + F)
+    R = B * ((v.image_size // v.patch_size) ** 2 + 1)
+    D, F = v.hidden_size, v.intermediate_size
+    Kp = 3 * v.patch_size ** 2
+    Kp = (Kp + 63) // 64 * 64 if Kp % 8 else Kp
+    fwd = [(R, D, Kp, 0)]
+    for _ in range(v.num_hidden_layers):
+        fwd += [(R, 3 * D, D, 0), (R, D, D, R * D * 2), (R, F, D, R * F * 2 if train else 0), (R, D, F, R * D * 2)]
+    dgrad, wgrad = [], []
+    if train:
+        for _ in range(v.num_hidden_layers):
+            dgrad += [(R, F, D, R * F * 2), (R, D, F, 0), (R, D, D, 0), (R, D, 3 * D, 0)]
+            wgrad += [(D, F, R), (F, D, R), (D, D, R), (3 * D, D, R)]
+        wgrad.append((D, Kp, R))
+    return fwd + dgrad, wgrad
+
+
+def algorithmic_bytes(cfg, B, train):
+    """Mean compulsory HBM bytes per launch of each GEMM family (bf16 operands read once, output
+    written once: bf16 for forward/dgrad, fp32 gradient for wgrad), vision tower launches."""
+    fd, wg = vision_gemm_shapes(cfg, B, train)
+    out = {"gemm256_fwd_dgrad": sum((M * K + N * K + M * N) * 2 + x for M, N, K, x in fd) / len(fd)}
+    if wg:
+        out["gemm256_wgrad"] = sum(K * (M + N) * 2 + M * N * 4 for M, N, K in wg) / len(wg)
+    return {k: round(v) for k, v in out.items()}
 
 
 def cpu_baseline(cfg, B, steps):
@@ -146,11 +166,57 @@ def cpu_baseline(cfg, B, steps):
                       f"median of {steps} steps after 1 warm-up, torch CPU threads={threads}"}
 
 
+def self_launch(args):
+    """`--gpus N` without a torch.distributed environment: start N ranks (one per GPU) through
+    torch.distributed.run from this process, which has not touched the GPU, and exit with its
+    code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:])}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def family_roofline(name, launches, cfg, B, train):
+    """launches: [(ms, flops)] of one family on the caller's stream inside the timed steps."""
+    if not launches:
+        return None
+    tot_ms = sum(m for m, _ in launches)
+    tot_fl = sum(f for _, f in launches)
+    ach = tot_fl / (tot_ms * 1e-3) / 1e12
+    res = {"bound": "mfma", "kernel": name, "labels": FAMILIES[name], "launches": len(launches),
+           "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
+           "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(ach / PEAK_BF16_TFLOPS, 4), "ms_per_step_caller_stream": None,
+           "traffic": None, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": None,
+           "algorithmic_bytes": algorithmic_bytes(cfg, B, train).get(name)}
+    tf = TRAFFIC_FILES.get(name)
+    if tf and os.path.isfile(os.path.join(REPO, tf)):
+        try:
+            tj = json.load(open(os.path.join(REPO, tf)))
+            if tj.get("kernel") == name and (tj.get("workload") in (None, f"{cfg.name}/{B}/{int(train)}")):
+                res["traffic"], res["traffic_source"] = tj["bytes_per_launch"], tf
+        except (OSError, ValueError, KeyError):
+            pass
+    return res
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        print(json.dumps({"rank": rank, "world": world}), flush=True)
+        return
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
@@ -167,13 +233,12 @@ def main():
 
     cfg = C.resolve(args.model)
     adapters = args.mode == "adapter"
-    if args.roofline_kernel is None:
-        args.roofline_kernel = "gemm256_fwd_bias_qgelu" if adapters else "gemm256_wgrad_splitk"
     model = CLIPWithAdapters(args.model, use_text_adapter=adapters, use_vision_adapter=adapters,
                              use_shared_adapters=False, freeze_clip=adapters, device=dev, precision="bf16",
                              fast_init=True, process_group=group)
     params = [p for n, p in model.named_parameters() if p.requires_grad]
-    opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas())
+    opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas(), process_group=group)
+    opt.overlap_with(model)  # world > 1: gradient buckets all-reduced under the backward
     batch = synthetic_batch(cfg, args.batch, rank, dev)
     total = args.warmup + args.steps
 
@@ -201,8 +266,10 @@ def main():
     L = _lib.lib()
     L.clipmi_prof_arm.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.clipmi_prof_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
-    cap = 4096
-    _lib.check(L.clipmi_prof_arm(args.roofline_kernel.encode(), cap), "prof_arm")
+    L.clipmi_prof_read_labels.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    cap = 16384
+    labels = [lab for fam in FAMILIES.values() for lab in fam]
+    _lib.check(L.clipmi_prof_arm(",".join(labels).encode(), cap), "prof_arm")
     # only the caller's stream: the text tower's launches run on a second stream beside the
     # vision tower's kernels (model.py), so their event spans include the other tower's work
     L.clipmi_prof_stream.argtypes = [ctypes.c_void_p]
@@ -229,7 +296,9 @@ def main():
     L.clipmi_prof_disarm()
     ms = (ctypes.c_float * cap)()
     fl = (ctypes.c_double * cap)()
+    wh = (ctypes.c_int * cap)()
     n = L.clipmi_prof_read(cap, ms, fl)
+    L.clipmi_prof_read_labels(cap, wh)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -238,31 +307,23 @@ def main():
     value = pairs / elapsed
     fwd = C.forward_flops_per_pair(cfg)
     step_flops_pair = 3 * fwd if not adapters else fwd
-    roof = None
-    traffic, traffic_src = None, None
-    # HBM bytes per launch of the same kernel family from the committed PMC passes
-    # (tools/traffic_pmc.sh -> profiles/*_traffic.json; newest file wins)
-    import glob
-    tfiles = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=os.path.getmtime)
-    for tf in reversed(tfiles):
-        try:
-            tj = json.load(open(tf))
-        except (OSError, ValueError):
-            continue
-        if tj.get("kernel") == args.roofline_kernel:
-            traffic, traffic_src = tj["bytes_per_launch"], os.path.relpath(tf, REPO)
-            break
-    if n > 0:
-        avg_ms = sum(ms[i] for i in range(n)) / n
-        avg_fl = sum(fl[i] for i in range(n)) / n
-        ach = avg_fl / (avg_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": args.roofline_kernel, "launches": n,
-                "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": avg_fl,
-                "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                "algorithmic_bytes": (fc1_algorithmic_bytes(cfg, args.batch) if adapters
-                                      else wgrad_algorithmic_bytes(cfg, args.batch))}
+    per_fam = {name: [] for name in FAMILIES}
+    for i in range(n):
+        lab = labels[wh[i]]
+        for name, labs in FAMILIES.items():
+            if lab in labs:
+                per_fam[name].append((ms[i], fl[i]))
+    roofs = {}
+    for name in FAMILIES:
+        r = family_roofline(name, per_fam[name], cfg, args.batch, not adapters)
+        if r is not None:
+            r["ms_per_step_caller_stream"] = round(sum(m for m, _ in per_fam[name]) / args.steps, 2)
+            roofs[name] = r
+    if args.roofline_family and args.roofline_family in roofs:
+        main_fam = args.roofline_family
+    else:  # the dominant GEMM family by measured time
+        gem = {k: v for k, v in roofs.items() if k.startswith("gemm")}
+        main_fam = max(gem, key=lambda k: gem[k]["ms_per_step_caller_stream"]) if gem else None
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
@@ -277,7 +338,8 @@ def main():
         "mfma_frac_step": round(value * step_flops_pair / (world * PEAK_BF16_TFLOPS * 1e12), 4),
         "step_tflops_per_gpu": round(value * step_flops_pair / world / 1e12, 1),
         "loss": round(float(loss.item()), 4),
-        "roofline": roof,
+        "roofline": roofs.get(main_fam) if main_fam else None,
+        "rooflines": {k: v for k, v in roofs.items() if k != main_fam},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -103,7 +103,8 @@ int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, 
 /* The input step (CLIPImageProcessor's center_crop + rescale + normalize, [HF]
  * image_processing_clip.py) fused into the same im2col: uint8 images [B, Hin, Win, 3]
  * (channels last), centre-cropped to image_size, (u/255 - mean[c]) / std[c].  Resizing
- * stays on the host.  P % 8 == 0, Kp == 3*P*P; mean/std are 3 host floats. */
+ * stays on the host.  P even (16/32: 8 pixels per thread; ViT-L/14: 2), Kp == 3*P*P or padded
+ * to a multiple of 8 (the pad columns are zeroed: L/14's 588 -> 640); mean/std are 3 host floats. */
 int clipmi_im2col_u8(void* stream, int dtype, const uint8_t* images, void* X, int B, int Hin, int Win, int image_size,
                      int P, int Kp, const float* mean, const float* std);
 /* pooled token per row: mode 0 first token (model_m.py:102), 1 first EOS, 2 argmax id ([HF] :561-581) */
@@ -147,6 +148,9 @@ int clipmi_encoder_fwd(void* stream, const clipmi_encoder_desc* d);
 int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d);
 /* dx: dL/d(encoder output) in, dL/d(encoder input) out */
 int clipmi_encoder_bwd(void* stream, const clipmi_encoder_desc* d, void* dx);
+/* the same for layers layer_hi-1 .. layer_lo only (chunked backward: each chunk's gradient slice
+ * can be all-reduced while the next chunk runs) */
+int clipmi_encoder_bwd_layers(void* stream, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo);
 
 /* ---- Contrastive head (model_m.py:146-171), fp32 -------------------------------------------- */
 int clipmi_l2norm_fwd(void* stream, const float* x, float* y, float* nrm, int B, int E);
@@ -208,11 +212,13 @@ int clipmi_softmax_rows(void* stream, const float* x, float* y, int R, int N, fl
 int clipmi_softmax_rows_bwd(void* stream, const float* y, const float* dy, float* dx, int R, int N, float scale);
 
 /* ---- Live kernel timing (bench.py roofline) --------------------------------------------------
- * While armed, every launch whose variant label equals `variant` (e.g. "gemm_fwd_bias_qgelu_pre",
- * "gemm_wgrad_splitk", "attn_fwd", "attn_bwd") is bracketed by hipEvents on its own stream,
- * up to max_launches.  clipmi_prof_read (after a synchronize) returns the launch count and
- * fills per-launch milliseconds and algorithmic FLOPs. */
-int clipmi_prof_arm(const char* variant, int max_launches);
+ * While armed, every launch whose variant label is in the comma-separated list `variants`
+ * (e.g. "gemm256_fwd_bias_qgelu_pre,gemm256_dgrad", "gemm256_wgrad", "attn_fwd") is bracketed by
+ * hipEvents on its own stream, up to max_launches.  clipmi_prof_read (after a synchronize)
+ * returns the launch count and fills per-launch milliseconds and algorithmic FLOPs;
+ * clipmi_prof_read_labels gives each launch's index in the list. */
+int clipmi_prof_arm(const char* variants, int max_launches);
+int clipmi_prof_read_labels(int max, int* which);
 int clipmi_prof_disarm(void);
 /* Restrict the armed profiler to launches on one HIP stream (which may be the null stream):
  * with the towers on

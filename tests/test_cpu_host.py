@@ -228,3 +228,63 @@ def test_shared_adapter_state_dict_schema():
     names = [n for n, _ in m.named_parameters() if "shared_adapters" in n]
     assert len(names) == 2 * len(want) and all("adapter" in n for n in names)
     assert len(m.arenas()) == 5
+
+
+def _reducer_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from clipmi.arena import Arena
+    from clipmi.trainer import GradBucketReducer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = Arena([("w0", (300,)), ("w1", (17, 9)), ("w2", (1000,))], "cpu", dtype_shadow=False)
+    b = Arena([("v", (70,))], "cpu", dtype_shadow=False)
+    g = torch.Generator().manual_seed(rank)
+    a.grad.copy_(torch.randn(a.numel, generator=g))
+    b.grad.copy_(torch.randn(b.numel, generator=g))
+    r = GradBucketReducer([a, b], dist.group.WORLD)
+    # two buckets reported out of order (as a chunked backward does), the rest left to finish()
+    r.ready(a, a.offsets["w2"][0], 1000)
+    r.ready(a, 64, 128)
+    r.finish()
+    q.put((rank, a.grad.numpy().copy(), b.grad.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_grad_bucket_reducer_sums_every_element_once_gloo():
+    """GradBucketReducer (SURVEY §8e bucketed, overlapped all-reduce): reported buckets plus the
+    complement finish() reduces = exactly one all-reduce of every arena element."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+    from clipmi.arena import Arena
+    want_a, want_b = 0, 0
+    for rank in range(2):
+        g = torch.Generator().manual_seed(rank)
+        a = Arena([("w0", (300,)), ("w1", (17, 9)), ("w2", (1000,))], "cpu", dtype_shadow=False)
+        b = Arena([("v", (70,))], "cpu", dtype_shadow=False)
+        want_a = want_a + torch.randn(a.numel, generator=g)
+        want_b = want_b + torch.randn(b.numel, generator=g)
+    for rank, ga, gb in res:
+        np.testing.assert_allclose(ga, want_a.numpy(), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(gb, want_b.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_bench_self_launches_n_ranks():
+    """`bench.py --gpus 2` with no torch.distributed environment starts 2 ranks itself (through
+    torch.distributed.run, before any GPU call); --launch-check stops each rank before the GPU."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted((d["rank"], d["world"]) for d in lines) == [(0, 2), (1, 2)]

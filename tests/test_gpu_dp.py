@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=False):
     import sys
     sys.path.insert(0, os.path.join(REPO, "vlm-clip_amd"))
     import torch.distributed as dist
@@ -27,7 +27,11 @@ def _worker(rank, world, port, q):
                          process_group=dist.group.WORLD)
     B = 4
     b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
-    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas())
+    if overlap:  # gradient buckets all-reduced from the towers' chunked backward (GradBucketReducer)
+        opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas(),
+                         process_group=dist.group.WORLD).overlap_with(m)
+    else:
+        opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas())
     opt.zero_grad()
     out = m(**b)
     out["loss"].backward()
@@ -39,13 +43,15 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_data_parallel_matches_single_device():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_two_rank_data_parallel_matches_single_device(overlap):
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port += 37 * int(overlap)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])

@@ -272,3 +272,38 @@ def test_im2col_uint8_matches_processor(golden, tag, dtype, P):
     torch.cuda.synchronize()
     tol = 2e-6 if dtype == torch.float32 else 2e-2
     assert (X.float() - Xr.float()).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("tag,D,ln", [("text", 512, True), ("vision", 768, True), ("textual", 512, False)])
+def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln):
+    """towers.AdapterFn on every token of [2, 5, D] (TextAdapter / VisionAdapter, and with ln=False
+    peclip.TextualAdapter, adapter/peclip.py:13-18) through libclipmi: output, input gradient and
+    parameter gradients vs the reference modules' run (tests/golden/adapters.npz)."""
+    import types
+    from clipmi import synth
+    from clipmi import towers as T
+    from clipmi.modules import AdapterParams
+    g = golden("adapters.npz")
+    names = ("down_project", "up_project") if ln else ("down_proj", "up_proj")
+    mod = AdapterParams(D, 256, "cuda", ln=ln, shadow=precision == "bf16", names=names)
+    sd = synth.adapter_state_dict(D, 256, 7, f"{tag}_adapter", ln=ln)
+    if not ln:
+        sd = {k.replace("down_project", "down_proj").replace("up_project", "up_proj"): v for k, v in sd.items()}
+    mod.load_numpy(sd)
+    dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+    rt = types.SimpleNamespace(dtype=dtype)
+    x = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/x")).cuda().requires_grad_(True)
+    gy = torch.from_numpy(synth.normal((2, 5, D), 7, f"{tag}/gy")).cuda()
+    anchor = next(iter(mod.parameters()))
+    y = T.AdapterFn.apply(x, anchor, rt, mod, True)
+    y.float().backward(gy)
+    torch.cuda.synchronize()
+    tol = 1e-4 if precision == "fp32" else 5e-2
+
+    def rel(a, b):
+        return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
+    assert rel(y.detach().float().cpu().numpy(), g[f"{tag}_y"]) < tol
+    assert rel(x.grad.float().cpu().numpy(), g[f"{tag}_gx"]) < tol
+    for k, p in mod.named_parameters():
+        assert rel(p.grad.cpu().numpy(), g[f"{tag}_g/{k}"]) < (tol if precision == "fp32" else 0.1), k

@@ -179,3 +179,77 @@ def test_shared_adapters_oracle_matches_reference(golden):
     with torch.no_grad():
         f = R.text_features(b["input_ids"], b["attention_mask"], p, cfg, ta, shared_adapters=sh)
     np.testing.assert_allclose(f.numpy(), g["text_features_raw"], atol=2e-5, rtol=1e-4)
+
+
+def sampled_grads(g):
+    """name -> (kind, ref, idx) for the sampled gradients of tools/gen_goldens._grad_sample."""
+    out = {}
+    for k in g.files:
+        if k.startswith("grad/"):
+            out[k[5:]] = ("full", g[k], None)
+        elif k.startswith("grad_head/"):
+            out[k[10:]] = ("head", g[k], None)
+        elif k.startswith("grad_rows/"):
+            out[k[10:]] = ("rows", g[k], g["grad_rows_idx/" + k[10:]])
+    return out
+
+
+def take_sample(kind, t, idx):
+    if kind == "full":
+        return t
+    if kind == "head":
+        return t.reshape(t.shape[0], -1)[:8]
+    return t[idx]
+
+
+def test_b16_full_finetune_gradients(golden):
+    """BASELINE config 3's workload (ViT-B/16 full fine-tune) at B=2: oracle loss backward vs the
+    reference's, every parameter (sampled rows, tools/gen_goldens.gen_b16_full_grads)."""
+    g = golden("forward_b16_full_grads.npz")
+    cfg = C.resolve("B/16")
+    torch.set_num_threads(8)
+    p, _, _ = model_params(cfg, False, requires_grad=True)
+    out = R.clip_with_adapters_forward(batch(cfg, 2, g), p, cfg)
+    out["loss"].backward()
+    np.testing.assert_allclose(out["loss"].item(), g["loss"], atol=1e-5)
+    s = sampled_grads(g)
+    assert len(s) == len(p) - 2  # every tensor but post_layernorm (unused, quirk Q2)
+    gmax = max(float(np.abs(r).max()) for _, r, _ in s.values())
+    for n, (kind, ref, idx) in s.items():
+        got = take_sample(kind, p[n].grad, idx).numpy()
+        scale = max(float(np.abs(ref).max()), 0.05 * gmax, 1e-8)
+        assert float(np.abs(got - ref).max()) / scale < 1e-3, n
+
+
+def test_shared_adapters_unfrozen_position_embedding_grad(golden):
+    """Unfrozen CLIP + shared adapters: the vision position embedding's gradient through the
+    adapters' keys/values (model_m.py:96-100), oracle vs the reference run caption by caption."""
+    g = golden("shared_adapters_unfrozen.npz")
+    cfg = C.resolve("B/32")
+    p, ta, _ = model_params(cfg, True, requires_grad=True)
+    t, v = cfg.text_config, cfg.vision_config
+    sh = [R.to_torch(synth.shared_adapter_state_dict(t.hidden_size, v.hidden_size, 0, f"shared_adapters.{i}"),
+                     requires_grad=True) for i in range(2)]
+    b = batch(cfg, 4, g)
+    G = torch.from_numpy(synth.normal((4, cfg.projection_dim), 11, "shared_G"))
+    f = R.text_features(b["input_ids"], b["attention_mask"], p, cfg, ta, shared_adapters=sh)
+    (f * G).sum().backward()
+    np.testing.assert_allclose(f.detach().numpy(), g["text_features_raw"], atol=2e-5, rtol=1e-4)
+    for n, got in (("vision_model.embeddings.position_embedding.weight", p["vision_model.embeddings.position_embedding.weight"].grad),
+                   ("text_projection.weight", p["text_projection.weight"].grad),
+                   ("shared_adapters.0.image_proj.weight", sh[0]["image_proj.weight"].grad),
+                   ("shared_adapters.1.norm1.weight", sh[1]["norm1.weight"].grad)):
+        ref = g["grad/" + n]
+        assert float(np.abs(got.numpy() - ref).max()) / float(np.abs(ref).max()) < 1e-4, n
+
+
+def test_b32_adapter_b256_forward(golden):
+    """BASELINE config 2's batch (B/32 + adapters, B=256): oracle forward vs the reference."""
+    g = golden("forward_b32_adapter_b256.npz")
+    cfg = C.resolve("B/32")
+    torch.set_num_threads(8)
+    p, ta, va = model_params(cfg, True)
+    with torch.no_grad():
+        out = R.clip_with_adapters_forward(batch(cfg, 256, g), p, cfg, ta, va)
+    np.testing.assert_allclose(out["logits_per_text"].numpy(), g["logits_per_text"], atol=1e-4)
+    np.testing.assert_allclose(out["loss"].item(), g["loss"], atol=1e-5)

@@ -136,6 +136,93 @@ def gen_forward(preset, B, tag, adapters=True, grads=False, layer=False, freeze_
     save(f"forward_{tag}.npz", **out)
 
 
+def _grad_sample(name, g, ids=None):
+    """A bounded sample of a big gradient: 1-D tensors whole, others their first 8 rows (the
+    token embedding: the rows of the ids the batch uses, which are its only non-zero rows)."""
+    out = {}
+    if g.ndim <= 1:
+        out[f"grad/{name}"] = g
+    elif name.endswith("token_embedding.weight") and ids is not None:
+        used = np.unique(ids)[:16]
+        out[f"grad_rows/{name}"] = g[used]
+        out[f"grad_rows_idx/{name}"] = used.astype(np.int64)
+    else:
+        out[f"grad_head/{name}"] = g.reshape(g.shape[0], -1)[:8]
+    return out
+
+
+def gen_b16_full_grads():
+    """BASELINE config 3's workload at parity size: ViT-B/16 full fine-tune (adapters off, every CLIP
+    parameter + logit_scale trainable, quirk Q4), the reference's loss backward at B=2.  Gradients
+    are sampled per tensor (_grad_sample) to keep the fixture small."""
+    cfg = C.resolve("B/16")
+    ref = build_reference_model(cfg, False, False, freeze_clip=False)
+    b_np, b = batch_tensors(cfg, 2)
+    ref.train()  # no dropout on this path (attention_dropout = 0)
+    res = ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=b["pixel_values"])
+    res["loss"].backward()
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"]))}
+    for k in ("loss", "logits_per_text", "text_features", "image_features"):
+        out[k] = res[k].detach().numpy()
+    n = 0
+    for k, p in ref.named_parameters():
+        if p.grad is not None:
+            out.update(_grad_sample(k[5:] if k.startswith("clip.") else k, p.grad.numpy(), b_np["input_ids"]))
+            n += 1
+    print("b16 full grads: tensors", n)
+    save("forward_b16_full_grads.npz", **out)
+
+
+def gen_b32_adapter_b256():
+    """BASELINE config 2's batch at parity: ViT-B/32 + text/vision adapters (A=256, shared off), frozen
+    towers, B=256: features, logits, loss and the adapter gradients (the trainable set)."""
+    cfg = C.resolve("B/32")
+    ref = build_reference_model(cfg, True, True, freeze_clip=True)
+    b_np, b = batch_tensors(cfg, 256)
+    ref.train()
+    res = ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=b["pixel_values"])
+    res["loss"].backward()
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"]))}
+    for k in ("loss", "logits_per_text", "text_features", "image_features"):
+        out[k] = res[k].detach().numpy()
+    for k, p in ref.named_parameters():
+        if p.grad is not None:
+            out[f"grad/{k}"] = p.grad.numpy()
+    save("forward_b32_adapter_b256.npz", **out)
+
+
+def gen_shared_unfrozen():
+    """gen_shared with the CLIP parameters unfrozen: the shared adapters' keys/values come from the
+    vision position embedding (model_m.py:96-100), so its gradient must include that path.  Batch-1
+    runs per caption (quirk Q3), L = sum_b <features_b, G_b>; records the position-embedding gradient
+    and the text projection's."""
+    cfg = C.resolve("B/32")
+    import model_m
+    ref = build_reference_model(cfg, True, True, freeze_clip=False)
+    t, v = cfg.text_config, cfg.vision_config
+    ref.use_shared_adapters = True
+    ref.shared_adapters = torch.nn.ModuleList([model_m.SharedMHSAttentionAdapter(t.hidden_size, v.hidden_size)
+                                               for _ in range(2)])
+    for i, sa in enumerate(ref.shared_adapters):
+        sa.load_state_dict({k: torch.from_numpy(x) for k, x in synth.shared_adapter_state_dict(
+            t.hidden_size, v.hidden_size, 0, f"shared_adapters.{i}").items()})
+    ref.eval()
+    b_np, b = batch_tensors(cfg, 4)
+    G = torch.from_numpy(synth.normal((4, cfg.projection_dim), 11, "shared_G"))
+    feats = []
+    for i in range(4):
+        f = ref.get_text_features(b["input_ids"][i:i + 1], b["attention_mask"][i:i + 1])
+        (f * G[i:i + 1]).sum().backward()
+        feats.append(f.detach())
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"])),
+           "text_features_raw": torch.cat(feats).numpy()}
+    named = dict(ref.named_parameters())
+    for k in ("clip.vision_model.embeddings.position_embedding.weight", "clip.text_projection.weight",
+              "shared_adapters.0.image_proj.weight", "shared_adapters.1.norm1.weight"):
+        out[f"grad/{k[5:] if k.startswith('clip.') else k}"] = named[k].grad.numpy()
+    save("shared_adapters_unfrozen.npz", **out)
+
+
 def gen_l14():
     """Config 4's model: ViT-L/14 (P=14 -> patch K=588, N=257 tokens) + adapters, frozen towers, with the
     adapter gradients (the trainable set of the adapter fine-tune)."""

@@ -236,7 +236,14 @@ class CLIPAdapter:
                                                                            False)
 
     def train_step(self, pixel_values, labels, learning_rate, temperature):
-        """One iteration of model_t.py:165-218 (features -> adapters -> logits -> CE -> Adam)."""
+        """One iteration of model_t.py:165-218 (features -> adapters -> logits -> CE -> Adam).
+        Labels are validated on the host first: torch's CrossEntropyLoss raises before
+        optimizer.step(), so a bad batch must leave both adapters untouched."""
+        lab = torch.as_tensor(labels).detach().to("cpu", torch.int64)
+        C = self.emotion_embedding_tensor.shape[0]
+        bad_lab = lab[(lab < 0) | (lab >= C)]
+        if bad_lab.numel():
+            raise IndexError(f"Target {int(bad_lab[0])} is out of bounds.")
         f = self.model.get_image_features(pixel_values)
         img, s_img = self.visual_adapter.blend(f, self.alpha, True)
         txt, s_txt = self.text_adapter.blend(self.emotion_embedding_tensor, self.beta, False)

@@ -34,6 +34,7 @@ class _Runtime:
         self.tenc = T.Encoder(self.arena, "text_model", self.cfg.text_config, causal=True)
         self.train_tower = False
         self.bad_flag = torch.zeros(1, dtype=torch.int32, device=self.arena.device)
+        self.grad_hook = None  # data-parallel gradient-ready hook (CLIPWithAdapters.set_grad_hook)
 
 
 def _anchor(module: nn.Module):
@@ -154,6 +155,11 @@ class CLIPWithAdapters(nn.Module):
         for param in self.clip.parameters():
             param.requires_grad = True
 
+    def set_grad_hook(self, fn):
+        """fn(arena, offset, numel) is called when a contiguous slice of a gradient arena is
+        final for this backward (trainer.GradBucketReducer.ready); None disables it."""
+        self._rt.grad_hook = fn
+
     @property
     def dtype(self):
         return self._rt.dtype
@@ -215,9 +221,11 @@ class CLIPWithAdapters(nn.Module):
         if self.use_shared_adapters:
             # model_m.py:95-100: image tokens = the vision position embedding, shared by the batch
             from .shared_adapter import SharedAdapterFn
-            pos = self.clip.arena.view("vision_model.embeddings.position_embedding.weight")
+            # the Parameter itself, so an unfrozen CLIP gets this path's position-embedding gradient
+            pos = self.clip.vision_model.embeddings.position_embedding.weight
             for sa in self.shared_adapters:
-                h = SharedAdapterFn.apply(h, _anchor(sa), sa, pos, self._adapter_needs_grad(sa, h))
+                need = self._adapter_needs_grad(sa, h) or (torch.is_grad_enabled() and pos.requires_grad)
+                h = SharedAdapterFn.apply(h, _anchor(sa), sa, pos, need)
         return T.PoolProjFn.apply(h, self.clip.text_projection.weight, self._rt, "text_projection.weight", idx)
 
 
@@ -255,6 +263,8 @@ class CLIPWithAdapters(nn.Module):
             return False
         if not torch.is_grad_enabled() or not self.clip.arena.any_requires_grad():
             return True
+        if self.use_shared_adapters:  # the text branch then also writes a vision parameter's gradient
+            return False
         return self.clip.logit_scale.requires_grad
 
     def _side_stream(self):

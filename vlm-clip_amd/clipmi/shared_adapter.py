@@ -81,6 +81,10 @@ class SharedAdapterFn(torch.autograd.Function):
         a = mod.arena
         W = lambda n: a.view(n)  # noqa: E731  (fp32 master weights)
         shp, dt = x.shape, x.dtype
+        if shp[-1] != mod.text_in:  # nn.Linear's error in text_proj (adapter/clip_adapter.py:101)
+            rows = x.numel() // max(1, shp[-1])
+            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({rows}x{shp[-1]} and "
+                               f"{mod.text_in}x{mod.hidden})")
         x32 = x.reshape(-1, mod.text_in).to(torch.float32).contiguous()
         img = image_tokens.to(torch.float32).contiguous()
         R, Nv, H, nh = x32.shape[0], img.shape[0], mod.hidden, mod.hidden // HEAD
@@ -181,13 +185,19 @@ class SharedAdapterFn(torch.autograd.Function):
         K.gemm(Nv, H, H, dk, H, True, Win[H:2 * H], H, False, dln1, H)
         K.gemm(Nv, H, H, dv, H, True, Win[2 * H:], H, False, dln1, H, flags=BETA)
         dt = _ln_bwd(dln2, t, st2, a.ptr("norm2.weight", a.data), gp("norm2.weight"), gp("norm2.bias"), R, H)
-        if train:
+        need_img = ctx.needs_input_grad[3]  # the vision position embedding trains (CLIP unfrozen)
+        dimg = None
+        if train or need_img:
             du = _ln_bwd(dln1, u, st1, a.ptr("norm1.weight", a.data), gp("norm1.weight"), gp("norm1.bias"), Nv, H)
+        if train:
             K.gemm(H, Dt, R, dt, H, False, x32, Dt, False, G("text_proj.weight"), Dt, flags=BETA)
             _colsum(dt, R, H, gp("text_proj.bias"))
             K.gemm(H, Dv, Nv, du, H, False, img, Dv, False, G("image_proj.weight"), Dv, flags=BETA)
             _colsum(du, Nv, H, gp("image_proj.bias"))
+        if need_img:  # d image_tokens = du @ image_proj.weight (model_m.py:96-100 backpropagates into it)
+            dimg = f(Nv, Dv)
+            K.gemm(Nv, Dv, H, du, H, True, W("image_proj.weight"), Dv, False, dimg, Dv)
         dx = f(R, Dt)
         K.gemm(R, Dt, H, dt, H, True, W("text_proj.weight"), Dt, False, dx, Dt)
         ctx.save = None
-        return dx.view(ctx.shape).to(ctx.dt), None, None, None, None
+        return dx.view(ctx.shape).to(ctx.dt), None, None, dimg, None

@@ -56,6 +56,7 @@ P = ctypes.POINTER
 _lib.declare("clipmi_encoder_fwd", [c_vp, P(EncoderDesc)])
 _lib.declare("clipmi_encoder_bwd", [c_vp, P(EncoderDesc), c_vp])
 _lib.declare("clipmi_encoder_bwd_ws", [P(EncoderDesc)], c_i64)
+_lib.declare("clipmi_encoder_bwd_layers", [c_vp, P(EncoderDesc), c_vp, c_int, c_int])
 _lib.declare("clipmi_layernorm_fwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                       c_float, c_vp, c_vp, c_int])
 _lib.declare("clipmi_layernorm_bwd_ws", [c_int, c_int], c_i64)
@@ -209,6 +210,38 @@ class Encoder:
         return d
 
 
+    def layer_range(self, lo, hi):
+        """(offset, numel) of layers lo..hi-1 in the arena: each layer's parameters are one
+        contiguous block (modules.layer_specs), consecutive layers adjacent."""
+        a = self.arena
+        start = a.offsets[f"{self.prefix}.encoder.layers.{lo}.layer_norm1.weight"][0]
+        off, _, n = a.offsets[f"{self.prefix}.encoder.layers.{hi - 1}.mlp.fc2.bias"]
+        return start, off + n - start
+
+    def backward(self, s, d, dx, hook):
+        """Encoder backward (layers L-1 .. 0).  With a gradient-ready hook (data-parallel runs)
+        it runs in chunks of layers and reports each chunk's gradient slice as soon as its
+        kernels are queued, so the all-reduce of the upper layers overlaps the lower layers'
+        backward; without one it is a single native call."""
+        L = self.t.num_hidden_layers
+        if hook is None:
+            _lib.check(_lib.lib().clipmi_encoder_bwd(s, ctypes.byref(d), dx), "clipmi_encoder_bwd")
+            return
+        step = max(1, (L + 3) // 4)
+        hi = L
+        while hi > 0:
+            lo = max(0, hi - step)
+            _lib.check(_lib.lib().clipmi_encoder_bwd_layers(s, ctypes.byref(d), dx, hi, lo), "clipmi_encoder_bwd_layers")
+            off, n = self.layer_range(lo, hi)
+            hook(self.arena, off, n)
+            hi = lo
+
+
+def _grad_hook(rt):
+    """The data-parallel gradient-ready hook (trainer.GradBucketReducer.ready) when one is active."""
+    return getattr(rt, "grad_hook", None)
+
+
 def _wbuf(arena, dtype):
     if dtype == torch.bfloat16:
         arena.sync_shadow()
@@ -290,7 +323,8 @@ class VisionTowerFn(torch.autograd.Function):
         d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads())
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
-        _lib.check(_lib.lib().clipmi_encoder_bwd(s, ctypes.byref(d), dx.data_ptr()), "clipmi_encoder_bwd")
+        hook = _grad_hook(rt)
+        rt.venc.backward(s, d, dx.data_ptr(), hook)
         # pre_layrnorm backward -> gradient of the embedding sum h0
         dh0 = torch.empty(R, D, dtype=dtype, device=dev)
         lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
@@ -314,6 +348,10 @@ class VisionTowerFn(torch.autograd.Function):
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
              arena.ptr("vision_model.embeddings.position_embedding.weight", g), 1)
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, 1, D, arena.ptr("vision_model.embeddings.class_embedding", g), 1)
+        if hook is not None:  # class / patch / position embeddings + pre_layrnorm: one contiguous block
+            lo = arena.offsets["vision_model.embeddings.class_embedding"][0]
+            hi = arena.offsets["vision_model.encoder.layers.0.layer_norm1.weight"][0]
+            hook(arena, lo, hi - lo)
         # activations are released with backward, not with the graph object (a caller holding
         # last step's loss would otherwise keep them alive into the next forward: 2x memory and
         # fresh device mallocs mid-step); stream-ordered reuse keeps the queued kernels safe
@@ -380,13 +418,16 @@ class TextTowerFn(torch.autograd.Function):
         d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads())
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
-        _lib.check(_lib.lib().clipmi_encoder_bwd(s, ctypes.byref(d), dx.data_ptr()), "clipmi_encoder_bwd")
+        hook = _grad_hook(rt)
+        rt.tenc.backward(s, d, dx.data_ptr(), hook)
         V = t.vocab_size
         ews = _ws(_lib.lib().clipmi_text_embed_bwd_ws(R, V), dev)
         call("clipmi_text_embed_bwd", s, dc, P_(ctx.ids), P_(dx), R, D, V,
              arena.ptr("text_model.embeddings.token_embedding.weight", g), 1, P_(ews), ews.numel())
         call("clipmi_period_sum", s, dc, P_(dx), D, B, S, S, D,
              arena.ptr("text_model.embeddings.position_embedding.weight", g), 1)
+        if hook is not None:  # token + position embeddings: the arena's first block
+            hook(arena, 0, arena.offsets["text_model.encoder.layers.0.layer_norm1.weight"][0])
         ctx.buf = ctx.acts = ctx.xL = ctx.stats = None  # released with backward (see VisionTowerFn)
         return None, None, None, None
 
@@ -487,11 +528,13 @@ class PoolProjFn(torch.autograd.Function):
         s = K.stream()
         dc = dcode(dtype)
         wbuf = _wbuf(arena, dtype)
+        W = arena.view(wname, wbuf)
+        E = W.shape[0]
+        if W.shape[1] != D:  # F.linear's error for the reference's text_projection(x) (model_m.py:103)
+            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({B}x{D} and {W.shape[1]}x{E})")
         hc = h.to(dtype).contiguous()
         pooled = torch.empty(B, D, dtype=dtype, device=dev)
         call("clipmi_gather_rows", s, dc, P_(hc), P_(idx), B, S, D, P_(pooled))
-        W = arena.view(wname, wbuf)
-        E = W.shape[0]
         out = torch.empty(B, E, dtype=torch.float32, device=dev)
         K.gemm(B, E, D, pooled, D, True, W, D, True, out, E)
         ctx.save = (pooled, idx)

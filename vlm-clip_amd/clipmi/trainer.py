@@ -26,13 +26,70 @@ def linear_schedule_with_warmup(step, warmup, total):
     return max(0.0, float(total - step) / float(max(1, total - warmup)))
 
 
+class GradBucketReducer:
+    """Data-parallel gradient sum, bucketed and overlapped with backward.
+
+    The towers report each finished chunk of encoder layers (a contiguous slice of the clip
+    arena's gradient) through ``ready``; its all-reduce is issued at once on a communication
+    stream that waits only for that slice's kernels, so it runs under the lower layers'
+    backward.  ``finish`` all-reduces whatever was not reported (projections, logit_scale,
+    final LNs, adapters) and makes the caller's stream wait for every bucket.  Each element is
+    reduced exactly once per step.  Collectives are issued from the autograd thread in node
+    order, which is the same on every rank."""
+
+    def __init__(self, arenas, group=None):
+        self.arenas = list(arenas)
+        self.group = group
+        self._ids = {id(a) for a in self.arenas}
+        self._done = {id(a): [] for a in self.arenas}
+        self._works = []
+        self._comm = None
+
+    def _comm_stream(self, dev):
+        if self._comm is None or self._comm.device != dev:
+            self._comm = torch.cuda.Stream(device=dev)
+        return self._comm
+
+    def _issue(self, t):
+        if t.is_cuda:
+            comm = self._comm_stream(t.device)
+            comm.wait_stream(torch.cuda.current_stream(t.device))
+            with torch.cuda.stream(comm):
+                self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+
+    def ready(self, arena, off, n):
+        if id(arena) not in self._ids or n <= 0:
+            return
+        self._done[id(arena)].append((off, off + n))
+        self._issue(arena.grad[off:off + n])
+
+    def finish(self):
+        for a in self.arenas:
+            pos = 0
+            for lo, hi in sorted(self._done[id(a)]):
+                if lo < pos:
+                    raise RuntimeError("GradBucketReducer: overlapping gradient buckets")
+                if lo > pos:
+                    self._issue(a.grad[pos:lo])
+                pos = hi
+            if pos < a.numel:
+                self._issue(a.grad[pos:a.numel])
+            self._done[id(a)] = []
+        for w in self._works:
+            w.wait()  # the caller's stream waits for the bucket's collective
+        self._works = []
+
+
 class FusedAdamW:
     """torch.optim.AdamW semantics (decoupled weight decay, bias-corrected) over arenas.
 
     An arena whose parameters are all trainable is updated by ONE launch; otherwise each
     trainable parameter's slice gets its own launch of the same kernel."""
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, arenas=()):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, arenas=(),
+                 process_group=None):
         params = list(params)
         if not params:
             raise ValueError("optimizer got an empty parameter list")
@@ -63,13 +120,25 @@ class FusedAdamW:
         self._gp = (ctypes.c_void_p * n)()
         self._gn = (ctypes.c_int64 * n)()
         self._norm_ws = torch.empty(int(_lib.lib().clipmi_grad_norm_multi_ws(n)), dtype=torch.uint8, device=dev)
+        self.reducer = None
+        if process_group is not None and dist.get_world_size(process_group) > 1:
+            self.reducer = GradBucketReducer(self.arenas, process_group)
+
+    def overlap_with(self, model):
+        """Report the model's gradient buckets to this optimizer's reducer during backward."""
+        model.set_grad_hook(self.reducer.ready if self.reducer is not None else None)
+        return self
 
     def zero_grad(self, set_to_none=False):
         for a in self.arenas:
             a.zero_grad()
 
     def grads_all_reduce(self, group=None):
-        """Data-parallel gradient sum: one RCCL all-reduce per arena (bucketed by layout)."""
+        """Data-parallel gradient sum: the overlapped buckets (GradBucketReducer) when this
+        optimizer was built with a process group, else one RCCL all-reduce per arena."""
+        if self.reducer is not None and (group is None or group is self.reducer.group):
+            self.reducer.finish()
+            return
         for a in self.arenas:
             dist.all_reduce(a.grad, group=group)
 
@@ -122,8 +191,12 @@ class CLIPAdapterTrainer:
                     self.trainable_params.append(param)
             elif param.requires_grad:
                 self.trainable_params.append(param)
+        pg = process_group
+        if pg is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            pg = dist.group.WORLD
         self.optimizer = FusedAdamW(self.trainable_params, lr=learning_rate, weight_decay=weight_decay,
-                                    arenas=model.arenas())
+                                    arenas=model.arenas(), process_group=pg)
+        self.optimizer.overlap_with(model)
         self.total_steps = None
 
     def _world(self):

@@ -167,6 +167,14 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
 // the encoder input (layer 0's x_in) on exit.  Grads accumulate into d->grads (fp32).
 extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* dx) {
   CLIPMI_TRY(validate(d));
+  return clipmi_encoder_bwd_layers(s, d, dx, d->L, 0);
+}
+
+// Layers layer_hi-1 down to layer_lo only: the data-parallel path calls the backward in chunks and
+// all-reduces each chunk's (contiguous) gradient slice while the next chunk computes.
+extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo) {
+  CLIPMI_TRY(validate(d));
+  CLIPMI_REQUIRE(0 <= layer_lo && layer_lo <= layer_hi && layer_hi <= d->L, "layer range");
   CLIPMI_REQUIRE(d->grads, "encoder_bwd needs gradient destinations");
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
@@ -195,7 +203,7 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
     if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
     return CLIPMI_OK;
   };
-  for (int l = d->L - 1; l >= 0; --l) {
+  for (int l = layer_hi - 1; l >= layer_lo; --l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
     const clipmi_layer_grad& g = d->grads[l];
