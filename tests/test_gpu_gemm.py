@@ -36,7 +36,8 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("akm,bkm", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("small", [0, 1, 4, 11])  # production (ping-pong 256), 128 tile, single-group 256, half-tile pipeline
+# production schedule, 128 tile, single-group 256, half-tile pipeline
+@pytest.mark.parametrize("small", [0, 1, 4, 11])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 136, 72), (77, 64, 768), (1000, 512, 200),
                                    (1000, 776, 768), (600, 264, 1000), (512, 256, 64), (520, 384, 96),
                                    (768, 256, 4160)])
@@ -66,7 +67,8 @@ def test_gemm_layouts(dtype, akm, bkm, M, N, K, small):
     _lib.EPI_BIAS, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, _lib.EPI_BIAS | _lib.EPI_GELU,
     _lib.EPI_BIAS | _lib.EPI_RESID, _lib.EPI_DQGELU, _lib.EPI_BETA])
 @pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
-def test_gemm_epilogues(flags, cdtype):
+@pytest.mark.parametrize("small", [0, 11])
+def test_gemm_epilogues(flags, cdtype, small):
     M, N, Kd = 300, 192, 256
     A = _mk((M, Kd), torch.bfloat16, 3)
     B = _mk((N, Kd), torch.bfloat16, 4)
@@ -77,7 +79,7 @@ def test_gemm_epilogues(flags, cdtype):
     cold = C.clone()
     aux_in = aux.clone()
     kern.gemm(M, N, Kd, A, Kd, True, B, Kd, True, C, N, bias=bias, residual=res, ldr=N, aux=aux, ldaux=N,
-           alpha=0.5, flags=flags)
+              alpha=0.5, flags=flags, small_tile=small)
     acc = A.float() @ B.float().t()
     ref, pre = _ref_epi(acc, flags, bias, aux_in, res, cold, alpha=0.5)
     torch.cuda.synchronize()

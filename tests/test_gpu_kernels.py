@@ -98,8 +98,16 @@ def attn_ref(qkv, B, N, H, mask, causal):
                                            # ViT-L/14 at 224 (N = 257) and the N <= 288 limit
                                            (2, 257, 16, False), (3, 288, 2, False), (40, 257, 16, False),
                                            # more (batch, head) items than the persistent grid
-                                           (90, 197, 12, False), (130, 77, 8, True)])
-def test_attention(dtype, B, N, H, causal):
+                                           (90, 197, 12, False), (130, 77, 8, True),
+                                           # ViT-L/14@336 (N = 577): K/V-streaming kernels
+                                           (2, 577, 4, False), (2, 400, 3, False), (3, 400, 2, True)])
+@pytest.mark.parametrize("fa", [False, True])
+def test_attention(dtype, B, N, H, causal, fa, monkeypatch):
+    """fa: the K/V-streaming flash forward (attn_fwd_fa) for every N (it is the only bf16 forward
+    for N > 288); otherwise the whole-K/V kernel where N allows."""
+    if fa and dtype == torch.float32:
+        pytest.skip("kernel choice applies to the bf16 path")
+    monkeypatch.setenv("CLIPMI_ATTN_FA", "1" if fa else "0")
     D = H * 64
     qkv = rnd((B * N, 3 * D), 11, dtype)
     mask = None
@@ -281,6 +289,7 @@ def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln):
     peclip.TextualAdapter, adapter/peclip.py:13-18) through libclipmi: output, input gradient and
     parameter gradients vs the reference modules' run (tests/golden/adapters.npz)."""
     import types
+    import numpy as np
     from clipmi import synth
     from clipmi import towers as T
     from clipmi.modules import AdapterParams
@@ -307,3 +316,29 @@ def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln):
     assert rel(x.grad.float().cpu().numpy(), g[f"{tag}_gx"]) < tol
     for k, p in mod.named_parameters():
         assert rel(p.grad.cpu().numpy(), g[f"{tag}_g/{k}"]) < (tol if precision == "fp32" else 0.1), k
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_attention_online_softmax_rescale(dtype, monkeypatch):
+    """cdna_hip_programming.md rule 26: force the deferred-max rescale branch of the streaming
+    forward.  Key 400 (tile 6 of 64) gets a score ~40 log2-units above the others for every
+    query, key 10 (tile 0) a moderate one; N = 577 runs the streamed kernels in both dtypes."""
+    monkeypatch.setenv("CLIPMI_ATTN_FA", "1")
+    B, N, H = 1, 577, 2
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 21, torch.float32)
+    q = qkv[:, :D].view(N, H, 64)
+    k = qkv[:, D:2 * D].view(N, H, 64)
+    u = rnd((H, 64), 22, torch.float32)
+    u = u / u.norm(dim=-1, keepdim=True)
+    q += 3.0 * u          # every query shares a component along u
+    k[400] = 30.0 * u     # scores ~ (3 + N(0,1)) * 3.75: ~15 log2 units above the rest
+    k[10] = 10.0 * u      # a smaller bump in the first tile
+    qkv = qkv.to(dtype).contiguous()
+    o = torch.empty(B * N, D, dtype=dtype, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    T.call("clipmi_attention_fwd", kern.stream(), DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), None, 0,
+           B, H, N, D)
+    oref, lref = attn_ref(qkv.float(), B, N, H, None, False)
+    assert rel(o, oref) < TOL[dtype], "O"
+    assert (lse - lref).abs().max().item() < (5e-2 if dtype == torch.bfloat16 else 1e-4), "lse"

