@@ -187,12 +187,25 @@ int clipmi_cast_f32_bf16(void* stream, const float* src, void* dst, int64_t n);
  * (1 - alpha) xn; out = z/|z|; rz = 1/|z|.  W1 [A, E], W2 [E, A] (nn.Linear layout). */
 int clipmi_feature_adapter_fwd(void* stream, const float* x, int B, int E, int A, const float* W1, const float* b1,
                                const float* W2, const float* b2, float alpha, int norm_in, float* xn, float* h,
-                               float* out, float* rz);
+                               float* out, float* rz, const uint8_t* keep, float keep_scale);
+/* keep (uint8 [B, A], may be NULL): training-mode nn.Dropout on the ReLU output (model_v.py:18-27:
+ * fc2(dropout(relu(fc1(x))))), h *= keep * keep_scale with keep_scale = 1/(1-p). */
 int clipmi_feature_adapter_bwd_ws(int B, int E, int A);
-/* grads = [dW1 | db1 | dW2 | db2] (flat, fp32) += the batch's gradients given dout = dL/dout. */
+/* grads = [dW1 | db1 | dW2 | db2] (flat, fp32) += the batch's gradients given dout = dL/dout;
+ * keep_scale: the forward's (1 when it ran without dropout). */
 int clipmi_feature_adapter_bwd(void* stream, const float* dout, const float* out, const float* rz, const float* xn,
                                const float* h, int B, int E, int A, const float* W2, float alpha, float* grads,
-                               void* workspace, int64_t workspace_bytes);
+                               void* workspace, int64_t workspace_bytes, float keep_scale);
+/* Dropout masks (nn.Dropout(p) in model_v.BaseAdapter and SharedMHSAttentionAdapter,
+ * adapter/clip_adapter.py:84,96): keep[i] = u(seed, offset + i) >= p with a counter-based hash,
+ * so a (seed, offset) pair reproduces its mask; apply: y = x * keep * scale (+ res, may be NULL). */
+int clipmi_dropout_mask(void* stream, uint8_t* keep, int64_t n, float p, uint64_t seed, uint64_t offset);
+int clipmi_dropout_apply(void* stream, const float* x, const uint8_t* keep, int64_t n, float scale, const float* res,
+                         float* y);
+/* Average fusion of model_v.EnhancedCLIPAdapter (model_v.py:310-315): out = normalise((a + b) / 2),
+ * ru = 1/|(a+b)/2|; backward d a = d b = dab. */
+int clipmi_fuse_avg(void* stream, const float* a, const float* b, int B, int E, float* out, float* ru);
+int clipmi_fuse_avg_bwd(void* stream, const float* dout, const float* out, const float* ru, int B, int E, float* dab);
 /* Class scores (model_t.py:200-203 logits, :240-247 predict, :252-298 predict_with_all_descriptions):
  * s[b, c] = max over descriptions j in [off[c], off[c+1]) of scale * img[b] . desc[j]; probs =
  * softmax_c.  Any output may be NULL.  With labels (int64 [B]): loss_rows[b] = CE of row b,

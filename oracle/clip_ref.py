@@ -148,10 +148,12 @@ def adapter(x, a, layer_norm_on=True, eps=1e-5):
     return h
 
 
-def shared_adapter(x, img, s, heads=8):
-    """SharedMHSAttentionAdapter.forward, adapter/clip_adapter.py:100-128 (eval mode), with the
-    image tokens img [N_v, D_v] broadcast over the batch (quirk Q3; the reference runs at B=1).
-    nn.MultiheadAttention core restated: q,k,v = in_proj; softmax(q k^T / sqrt(64)) v; out_proj."""
+def shared_adapter(x, img, s, heads=8, keep_p=None, keep_m=None, p=0.1):
+    """SharedMHSAttentionAdapter.forward, adapter/clip_adapter.py:100-128, with the image tokens
+    img [N_v, D_v] broadcast over the batch (quirk Q3; the reference runs at B=1).
+    nn.MultiheadAttention core restated: q,k,v = in_proj; softmax(q k^T / sqrt(64)) v; out_proj.
+    Training-mode dropout (p on the attention probabilities and on mlp.2's output, :84,96) when
+    masks are given: keep_p [heads, B*T, N_v], keep_m [B*T, hidden] (0/1)."""
     t = linear(x, s["text_proj.weight"], s["text_proj.bias"])
     u = linear(img, s["image_proj.weight"], s["image_proj.bias"])
     kv = layer_norm(u, s["norm1.weight"], s["norm1.bias"], 1e-5)
@@ -166,11 +168,18 @@ def shared_adapter(x, img, s, heads=8):
     qh = q.view(B, T, heads, hd).transpose(1, 2)
     kh = k.view(-1, heads, hd).transpose(0, 1)
     vh = v.view(-1, heads, hd).transpose(0, 1)
-    a = torch.softmax((qh @ kh.transpose(-1, -2)) * hd ** -0.5, dim=-1) @ vh
+    pr = torch.softmax((qh @ kh.transpose(-1, -2)) * hd ** -0.5, dim=-1)
+    if keep_p is not None:  # [heads, B*T, Nv] -> [B, heads, T, Nv]
+        kp = keep_p.to(pr.dtype).view(heads, B, T, -1).transpose(0, 1)
+        pr = pr * kp / (1.0 - p)
+    a = pr @ vh
     a = a.transpose(1, 2).reshape(B, T, H)
     hs = hs + linear(a, s["cross_attn.out_proj.weight"], s["cross_attn.out_proj.bias"])
     m = gelu_erf(linear(layer_norm(hs, s["norm3.weight"], s["norm3.bias"], 1e-5), s["mlp.0.weight"], s["mlp.0.bias"]))
-    return hs + linear(m, s["mlp.2.weight"], s["mlp.2.bias"])
+    z = linear(m, s["mlp.2.weight"], s["mlp.2.bias"])
+    if keep_m is not None:
+        z = z * keep_m.to(z.dtype).view(B, T, -1) / (1.0 - p)
+    return hs + z
 
 
 def text_features(input_ids, attention_mask, p, cfg, text_adapter=None, pooling="first", shared_adapters=None):

@@ -71,3 +71,49 @@ def zero_shot(img_feats, desc_n, protos, n_per_class):
     p = torch.softmax(100 * img @ protos.T, dim=1)
     s = (100 * img @ desc_n.T).view(img.shape[0], -1, n_per_class).amax(2)
     return p, torch.softmax(s, dim=1)
+
+
+# ---------------------------------------------------------------- model_v.EnhancedCLIPAdapter
+# model_v.py cannot be imported in the build container (qwen_vl_utils / bitsandbytes absent,
+# SURVEY §8c), so these functions restate it from source; their building blocks (adapter,
+# blend, class scores, Adam) are the model_t ones pinned above by tests/golden/heads.npz.  The
+# composition (context path, average fusion) is PARITY UNPINNED against a reference run.
+
+def adapter_dropout(x, W1, b1, W2, b2, keep=None, p=0.1):
+    """BaseAdapter.forward, model_v.py:25-26: fc2(dropout(relu(fc1(x)))); keep: the 0/1 mask."""
+    h = torch.relu(F.linear(x, W1, b1))
+    if keep is not None:
+        h = h * keep.to(h.dtype) / (1.0 - p)
+    return F.linear(h, W2, b2)
+
+
+def blend_v(x, w, alpha, norm_in, keep=None):
+    """model_v.py:269-285 (image: normalise first), :294-302 (context), :325-335 (text)."""
+    if norm_in:
+        x = x / x.norm(dim=-1, keepdim=True)
+    z = alpha * adapter_dropout(x, *w, keep=keep) + (1 - alpha) * x
+    return z / z.norm(dim=-1, keepdim=True)
+
+
+def enhanced_logits(img_feats, ctx, protos, wv, wt, wc, alpha, beta, gamma, temperature, keeps=(None, None, None)):
+    """EnhancedCLIPAdapter.forward, model_v.py:260-343 (training-mode text path: the text adapter
+    on the prototypes each call); keeps = (visual, context, text) dropout masks or None."""
+    img = blend_v(img_feats, wv, alpha, True, keeps[0])
+    comb = img
+    if ctx is not None and ctx.numel() > 0 and ctx.shape[-1] == img.shape[-1]:
+        c = blend_v(ctx, wc, gamma, False, keeps[1])
+        comb = (img + c) / 2.0                                  # :310-312
+        comb = comb / comb.norm(dim=-1, keepdim=True)            # :313-315
+    txt = blend_v(protos, wt, beta, False, keeps[2])
+    return temperature * comb @ txt.T                           # :340-342
+
+
+def enhanced_train_step(params, img_feats, ctx, protos, labels, alpha, beta, gamma, temperature, opt, keeps):
+    """main.py:66-86: CE(logits, labels) -> backward -> Adam over the three adapters."""
+    wv, wc, wt = params[:4], params[4:8], params[8:]
+    loss = F.cross_entropy(enhanced_logits(img_feats, ctx, protos, wv, wt, wc, alpha, beta, gamma, temperature, keeps),
+                           labels)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    return loss.detach()

@@ -143,3 +143,93 @@ def test_backbone_hf_feature_semantics(golden, precision, tol):
     ri, rt = g["hf_image_features"], g["text_eos_projected"]
     assert np.abs(fi - ri).max() / np.abs(ri).max() < tol
     assert np.abs(ft - rt).max() / np.abs(rt).max() < tol
+
+
+def _enhanced(g, ctx_dim=512):
+    """EnhancedCLIPAdapter over the fixture's feature tables, adapters initialised from the
+    heads.npz init weights (visual, text) and a seeded context adapter."""
+    desc, img, labels = fixture()
+    descs = {e: (torch.arange(i * 5, i * 5 + 5, device="cuda").view(5, 1), None) for i, e in enumerate(EMOS)}
+    m = HD.EnhancedCLIPAdapter(StubBackbone(desc, img), alpha=0.2, beta=0.2, gamma=0.3, bottleneck_dim=64,
+                               descriptions=descs, seed=3)
+    for nm, ad in (("visual", m.visual_adapter), ("text", m.text_adapter)):
+        ad.load_state_dict_(dict(zip(("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"), weights(g, "init", nm))))
+    ctx = torch.from_numpy(np.random.default_rng(4).standard_normal((24, ctx_dim)).astype(np.float32)).cuda()
+    return m, desc, img, labels, ctx
+
+
+def _w(ad):
+    sd = ad.state_dict_()
+    return [sd[k].clone() for k in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")]
+
+
+def test_enhanced_clip_adapter_eval_matches_oracle(golden):
+    """model_v.EnhancedCLIPAdapter eval path (model_v.py:260-353): logits and predict_probs with and
+    without context features vs oracle/heads_ref.enhanced_logits (no dropout in eval)."""
+    g = golden("heads.npz")
+    m, desc, img, labels, ctx = _enhanced(g)
+    m.eval()
+    m.encode_emotion_descriptions()
+    idx = torch.arange(24, device="cuda")
+    protos = torch.from_numpy(H.encode(torch.from_numpy(desc), 5)[1].numpy())
+    wv, wt, wc = _w(m.visual_adapter), _w(m.text_adapter), _w(m.context_adapter)
+    T = float(np.exp(LN100))
+    for c in (None, ctx):
+        got = m(idx, c).cpu()
+        ref = H.enhanced_logits(torch.from_numpy(img), None if c is None else c.cpu(), protos, wv, wt, wc, 0.2, 0.2,
+                                0.3, T)
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), atol=2e-3, rtol=1e-5)
+        pr = m.predict_probs(idx, c).cpu()
+        np.testing.assert_allclose(pr.numpy(), torch.softmax(ref, 1).numpy(), atol=1e-5)
+    # a context of the wrong width is skipped with a warning, as in the reference (:294-300)
+    bad = torch.zeros(24, 7, device="cuda")
+    np.testing.assert_allclose(m(idx, bad).cpu().numpy(), m(idx, None).cpu().numpy(), atol=1e-6)
+
+
+def test_enhanced_clip_adapter_training_matches_oracle_with_same_masks(golden):
+    """main.py:55-100 train loop (CE + Adam over visual/text/context adapters, dropout 0.1 in training
+    mode): 3 steps with context features; the oracle replays the same dropout masks (the seeded
+    counter generator makes them reproducible)."""
+    g = golden("heads.npz")
+    m, desc, img, labels, ctx = _enhanced(g)
+    m.eval()
+    m.encode_emotion_descriptions()
+    m.train()
+    protos = torch.from_numpy(H.encode(torch.from_numpy(desc), 5)[1].numpy())
+    params = [p.clone().requires_grad_(True) for p in _w(m.visual_adapter) + _w(m.context_adapter) + _w(m.text_adapter)]
+    opt = torch.optim.Adam(params, lr=3e-4)
+    T = float(np.exp(LN100))
+    lab = torch.from_numpy(labels)
+    for step in range(3):
+        sl = slice(8 * step, 8 * step + 8)
+        # the masks the three adapters will draw this step: visual [8, A], context [8, A], text [7, A]
+        keeps = []
+        for ad, n in ((m.visual_adapter, 8), (m.context_adapter, 8), (m.text_adapter, 7)):
+            d = HD.Dropout(ad.dropout.p, ad.dropout.seed)
+            d.offset = ad.dropout.offset
+            keeps.append(d.mask(n * ad.A, "cuda").view(n, ad.A).cpu())
+        loss = m.train_step(torch.arange(8 * step, 8 * step + 8, device="cuda"), lab[sl].cuda(), ctx[sl],
+                            learning_rate=3e-4)
+        ref = H.enhanced_train_step(params, torch.from_numpy(img[sl]), ctx[sl].cpu(), protos, lab[sl], 0.2, 0.2, 0.3,
+                                    T, opt, keeps)
+        assert abs(loss.item() - ref.item()) < 1e-4, (step, loss.item(), ref.item())
+    for ad, ref in ((m.visual_adapter, params[:4]), (m.context_adapter, params[4:8]), (m.text_adapter, params[8:])):
+        for got, r in zip(_w(ad), ref):
+            assert (got - r.detach()).abs().max().item() < 1e-4
+
+
+def test_dropout_masks_statistics_and_replay():
+    """Dropout(0.1) masks: ~10 % dropped, the kept values scaled by 1/0.9 keep the mean, and the same
+    (seed, offset) replays the same mask."""
+    d = HD.Dropout(0.1, 1234)
+    k1 = d.mask(1 << 20, "cuda").float()
+    frac = 1.0 - k1.mean().item()
+    assert abs(frac - 0.1) < 0.003, frac
+    x = torch.rand(1 << 20, device="cuda")
+    y = torch.empty_like(x)
+    HD.call("clipmi_dropout_apply", HD.T.K.stream(), x.data_ptr(), d.mask(1 << 20, "cuda").data_ptr(), x.numel(),
+            d.scale, None, y.data_ptr())
+    assert abs(y.mean().item() / x.mean().item() - 1.0) < 0.01
+    d2 = HD.Dropout(0.1, 1234)
+    assert torch.equal(d2.mask(1 << 20, "cuda").float(), k1)
+    assert not torch.equal(d2.mask(1 << 20, "cuda").float(), k1)  # the next draw differs

@@ -166,6 +166,7 @@ def test_shared_adapters_match_reference(golden, precision):
     runs at batch 1, quirk Q3), eval mode."""
     g = golden("shared_adapters.npz")
     m = CLIPWithAdapters("B/32", use_shared_adapters=True, freeze_clip=True, device="cuda", precision=precision)
+    m.eval()  # the reference ran in eval mode (no dropout)
     b = batch(m.config, 4, g)
     tf = m.get_text_features(b["input_ids"], b["attention_mask"])
     ref = g["text_features_raw"]
@@ -317,6 +318,7 @@ def test_shared_adapters_unfrozen_position_embedding_grad(golden):
     position embedding, model_m.py:96-100) must carry their gradient into that parameter."""
     g = golden("shared_adapters_unfrozen.npz")
     m = CLIPWithAdapters("B/32", use_shared_adapters=True, freeze_clip=False, device="cuda", precision="fp32")
+    m.eval()
     b = batch(m.config, 4, g)
     tf = m.get_text_features(b["input_ids"], b["attention_mask"])
     G = torch.from_numpy(synth.normal((4, m.config.projection_dim), 11, "shared_G")).cuda()
@@ -341,3 +343,52 @@ def test_projection_width_mismatch_raises():
     h = torch.zeros(2, 3, m.config.text_config.hidden_size + 64, device="cuda")
     with pytest.raises(RuntimeError, match="cannot be multiplied"):
         T.PoolProjFn.apply(h, m.clip.text_projection.weight, m._rt, "text_projection.weight", None)
+
+
+def test_shared_adapters_training_dropout_matches_oracle_with_same_masks():
+    """SharedMHSAttentionAdapter in training mode (dropout 0.1 on the attention probabilities and
+    after mlp.2, adapter/clip_adapter.py:84,96): features and adapter gradients vs the oracle fed the
+    masks the adapters drew (replayed from their seed/offset), fp32; and eval mode is unchanged."""
+    from oracle import clip_ref as R
+    from clipmi import towers as T
+    cfg = C.resolve("B/32")
+    m = CLIPWithAdapters("B/32", use_shared_adapters=True, freeze_clip=True, device="cuda", precision="fp32")
+    m.train()
+    b = batch(cfg, 4)
+    t, v = cfg.text_config, cfg.vision_config
+    nh, Hd, Nv, Rr = 8, 512, v.num_positions, 4
+    masks = []
+    for sa in m.shared_adapters:  # each layer draws [nh * R * Nv] then [R * H]
+        off = sa.drop_offset
+        kp = torch.empty(nh * Rr * Nv, dtype=torch.uint8, device="cuda")
+        km = torch.empty(Rr * Hd, dtype=torch.uint8, device="cuda")
+        T.call("clipmi_dropout_mask", T.K.stream(), kp.data_ptr(), kp.numel(), sa.p, sa.drop_seed, off)
+        T.call("clipmi_dropout_mask", T.K.stream(), km.data_ptr(), km.numel(), sa.p, sa.drop_seed, off + kp.numel())
+        masks.append((kp.view(nh, Rr, Nv).cpu(), km.view(Rr, Hd).cpu()))
+    tf = m.get_text_features(b["input_ids"], b["attention_mask"])
+    G = torch.from_numpy(synth.normal((4, cfg.projection_dim), 11, "shared_G")).cuda()
+    (tf * G).sum().backward()
+    torch.cuda.synchronize()
+    p = R.to_torch(synth.clip_state_dict(cfg, seed=0))
+    ta = R.to_torch(synth.adapter_state_dict(t.hidden_size, 256, 0, "text_adapter"))
+    sh = [R.to_torch(synth.shared_adapter_state_dict(t.hidden_size, v.hidden_size, 0, f"shared_adapters.{i}"),
+                     requires_grad=True) for i in range(2)]
+    bc = {k: x.cpu() for k, x in b.items()}
+    h = R.adapter(R.text_tower(bc["input_ids"], bc["attention_mask"], p, cfg), ta)[:, :1]
+    for s_, (kp, km) in zip(sh, masks):
+        h = R.shared_adapter(h, p["vision_model.embeddings.position_embedding.weight"], s_, keep_p=kp, keep_m=km)
+    ref = R.linear(h[:, 0], p["text_projection.weight"])
+    (ref * G.cpu()).sum().backward()
+    err = (tf.detach().cpu() - ref.detach()).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-4, err
+    params = dict(m.named_parameters())
+    for i in range(2):
+        for k, r in sh[i].items():
+            got = params[f"shared_adapters.{i}.{k}"].grad.cpu()
+            e = (got - r.grad).abs().max().item() / max(r.grad.abs().max().item(), 1e-8)
+            assert e < 1e-3, (i, k, e)
+    m.eval()
+    with torch.no_grad():
+        a1 = m.get_text_features(b["input_ids"], b["attention_mask"])
+        a2 = m.get_text_features(b["input_ids"], b["attention_mask"])
+    assert torch.equal(a1, a2)  # no dropout in eval mode

@@ -26,10 +26,14 @@ from . import towers as T
 
 c_vp, c_int, c_float, c_i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
 _lib.declare("clipmi_feature_adapter_fwd", [c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_int,
-                                            c_vp, c_vp, c_vp, c_vp])
+                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_float])
 _lib.declare("clipmi_feature_adapter_bwd_ws", [c_int, c_int, c_int])
 _lib.declare("clipmi_feature_adapter_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_float,
-                                            c_vp, c_vp, c_i64])
+                                            c_vp, c_vp, c_i64, c_float])
+_lib.declare("clipmi_dropout_mask", [c_vp, c_vp, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64])
+_lib.declare("clipmi_dropout_apply", [c_vp, c_vp, c_vp, c_i64, c_float, c_vp, c_vp])
+_lib.declare("clipmi_fuse_avg", [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp])
+_lib.declare("clipmi_fuse_avg_bwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp])
 _lib.declare("clipmi_class_scores", [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_float, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_vp])
 _lib.declare("clipmi_row_mean", [c_vp, c_vp, c_int, c_vp])
@@ -45,15 +49,36 @@ class _Linear:
         self.weight, self.bias = weight, bias
 
 
+class Dropout:
+    """nn.Dropout(p) masks from libclipmi's counter-based generator: each draw takes the next
+    `n` counters of (seed, offset), so a seed reproduces the whole sequence of masks."""
+
+    def __init__(self, p, seed):
+        self.p, self.seed, self.offset = float(p), int(seed) & (2 ** 63 - 1), 0
+
+    def mask(self, n, device):
+        keep = torch.empty(n, dtype=torch.uint8, device=device)
+        call("clipmi_dropout_mask", T.K.stream(), P_(keep), n, self.p, self.seed, self.offset)
+        self.offset += n
+        return keep
+
+    @property
+    def scale(self):
+        return 1.0 / (1.0 - self.p)
+
+
 class FeatureAdapter(nn.Module):
     """model_t.VisualAdapter / TextAdapter (:13-33): fc2(relu(fc1(x))), parameters in one flat
     fp32 buffer [fc1.weight | fc1.bias | fc2.weight | fc2.bias] so the gradient and the Adam
-    state are flat buffers too.  Initialised like nn.Linear (seeded), or from a state dict."""
+    state are flat buffers too.  Initialised like nn.Linear (seeded), or from a state dict.
+    dropout > 0 is model_v.BaseAdapter (:18-27): fc2(dropout(relu(fc1(x)))), active in
+    training mode (nn.Module.train / eval)."""
 
-    def __init__(self, input_dim, bottleneck_dim, device="cuda", seed=0):
+    def __init__(self, input_dim, bottleneck_dim, device="cuda", seed=0, dropout=0.0):
         super().__init__()
         E, A = input_dim, bottleneck_dim
         self.E, self.A = E, A
+        self.dropout = Dropout(dropout, seed * 7919 + 17) if dropout > 0 else None
         n = 2 * A * E + A + E
         self.flat = torch.zeros(n, dtype=torch.float32, device=device)
         self.grad = torch.zeros_like(self.flat)
@@ -99,24 +124,27 @@ class FeatureAdapter(nn.Module):
         xn, out = torch.empty_like(x), torch.empty_like(x)
         h = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
         rz = torch.empty(B, dtype=torch.float32, device=x.device)
+        keep, ks = None, 1.0
+        if self.dropout is not None and self.training:
+            keep, ks = self.dropout.mask(B * self.A, x.device), self.dropout.scale
         call("clipmi_feature_adapter_fwd", T.K.stream(), P_(x), B, self.E, self.A, P_(self.fc1.weight),
              P_(self.fc1.bias), P_(self.fc2.weight), P_(self.fc2.bias), float(alpha), int(norm_in), P_(xn), P_(h),
-             P_(out), P_(rz))
-        return out, (out, rz, xn, h, float(alpha))
+             P_(out), P_(rz), P_(keep), ks)
+        return out, (out, rz, xn, h, float(alpha), ks)
 
     def backward_(self, dout, saved):
         """grad += d loss / d params given dout = d loss / d out (accumulates, like autograd)."""
-        out, rz, xn, h, alpha = saved
+        out, rz, xn, h, alpha, ks = saved
         B = out.shape[0]
         ws = T._ws(_lib.lib().clipmi_feature_adapter_bwd_ws(B, self.E, self.A), out.device)
         call("clipmi_feature_adapter_bwd", T.K.stream(), P_(dout.contiguous()), P_(out), P_(rz), P_(xn), P_(h), B,
-             self.E, self.A, P_(self.fc2.weight), alpha, P_(self.grad), P_(ws), ws.numel())
+             self.E, self.A, P_(self.fc2.weight), alpha, P_(self.grad), P_(ws), ws.numel(), ks)
 
     def forward(self, x):
         """fc2(relu(fc1(x))) (model_t.py:22-23): the fused kernel at alpha = 1, no input
         normalisation, with its output normalisation undone (out / rz = z)."""
-        out, (_, rz, _, _, _) = self.blend(x, 1.0, False)
-        return out / rz[:, None]
+        out, saved = self.blend(x, 1.0, False)
+        return out / saved[1][:, None]
 
     def adam_step(self, lr, betas=(0.9, 0.999), eps=1e-8):
         self.step_count += 1
@@ -323,3 +351,151 @@ class ZeroShotEmotionRecognition:
 
     def predict_with_all_descriptions(self, pixel_values):
         return class_scores(self._image(pixel_values), self._bank.desc, self._bank.offsets, 100.0)[1]
+
+
+class ContextAdapter(FeatureAdapter):
+    """model_v.ContextAdapter (:30-31): the BaseAdapter bottleneck on VLM context features."""
+
+
+class EnhancedCLIPAdapter(nn.Module):
+    """model_v.EnhancedCLIPAdapter (:146-360) on libclipmi: visual / text / context BaseAdapters
+    (fc1 -> ReLU -> Dropout(0.1) -> fc2), alpha / beta / gamma residual blends with
+    renormalisation, average fusion of image and context features, logits = exp(logit_scale) *
+    fused . text^T, predict_probs = softmax; training (main.py:55-100) = CrossEntropy + Adam over
+    the three adapters, emotion embeddings refreshed after every epoch.
+
+    Every head operation runs in csrc/heads.hip (the fused adapter with its dropout mask, the
+    fusion, the class scores and CE, Adam).  The VLM context extractor (Qwen2.5-VL generation,
+    model_v.py:43-142) is outside this path: context features are passed to forward(), as the
+    reference's training loop does (main.py:68-77).  Descriptions arrive pre-tokenised
+    ({emotion: (input_ids, attention_mask)}; model_v uses one per emotion, "A person expressing
+    {emotion}", :204-206)."""
+
+    def __init__(self, clip_model_name, alpha=0.2, beta=0.2, gamma=0.3, bottleneck_dim=192, device="cuda",
+                 vlm_context_extractor=None, *, descriptions=None, precision="fp32", seed=0):
+        super().__init__()
+        self.device = device
+        self.model = _Backbone(clip_model_name, device, precision) if isinstance(clip_model_name, str) \
+            else clip_model_name
+        self.processor = None
+        dim = int(self.model.m.config.projection_dim if isinstance(self.model, _Backbone)
+                  else self.model.projection_dim)
+        self.image_feature_dim = self.text_feature_dim = dim
+        self.visual_adapter = FeatureAdapter(dim, bottleneck_dim, device, seed=seed, dropout=0.1)
+        self.text_adapter = FeatureAdapter(dim, bottleneck_dim, device, seed=seed + 1, dropout=0.1)
+        self.context_adapter = ContextAdapter(dim, bottleneck_dim, device, seed=seed + 2, dropout=0.1)
+        self.alpha, self.beta, self.gamma = alpha, beta, gamma
+        self.vlm_context_extractor = vlm_context_extractor
+        self.emotion_descriptions = descriptions
+        self.adapted_emotion_embedding_tensor = None
+        self.emotion_embedding_tensor = None
+
+    def _adapters(self):
+        return (self.visual_adapter, self.text_adapter, self.context_adapter)
+
+    def encode_emotion_descriptions(self, emotions=None):
+        """model_v.py:198-240: per emotion the mean of its normalised description features, then
+        update_emotion_embeddings()."""
+        if self.emotion_descriptions is None:
+            raise ValueError("descriptions {emotion: (input_ids, attention_mask)} are required (no tokenizer offline)")
+        descs = self.emotion_descriptions
+        if emotions is not None:
+            descs = {e: descs[e] for e in emotions}
+        self._bank = _DescriptionBank()
+        self._bank.encode(self.model, descs)
+        self.emotion_embedding_tensor = self._bank.protos
+        self.update_emotion_embeddings()
+
+    def update_emotion_embeddings(self):
+        """model_v.py:242-258 (in the module's current mode: dropout applies in training mode)."""
+        if self.emotion_embedding_tensor is None:
+            print("Warning: Original emotion embeddings not encoded. Call encode_emotion_descriptions first.")
+            return
+        self.adapted_emotion_embedding_tensor, _ = self.text_adapter.blend(self.emotion_embedding_tensor, self.beta,
+                                                                           False)
+
+    def _forward(self, pixel_values, context_features):
+        """(logits, state for backward); model_v.py:260-343."""
+        img_raw = self.model.get_image_features(pixel_values).float().contiguous()
+        img, s_img = self.visual_adapter.blend(img_raw, self.alpha, True)
+        combined, s_ctx, s_fuse = img, None, None
+        if context_features is not None and context_features.nelement() > 0:
+            if context_features.shape[-1] != self.text_feature_dim:
+                print(f"Warning: Context feature dimension mismatch. Expected {self.text_feature_dim}, "
+                      f"got {context_features.shape[-1]}. Skipping context.")
+            else:
+                ctx = context_features.to(device=img.device, dtype=torch.float32).contiguous()
+                ctx_f, s_ctx = self.context_adapter.blend(ctx, self.gamma, False)
+                combined = torch.empty_like(img)
+                ru = torch.empty(img.shape[0], dtype=torch.float32, device=img.device)
+                call("clipmi_fuse_avg", T.K.stream(), P_(img), P_(ctx_f), img.shape[0], img.shape[1], P_(combined),
+                     P_(ru))
+                s_fuse = (combined, ru)
+        s_txt = None
+        if self.training or self.adapted_emotion_embedding_tensor is None:
+            txt, s_txt = self.text_adapter.blend(self.emotion_embedding_tensor, self.beta, False)
+        else:
+            txt = self.adapted_emotion_embedding_tensor
+        temperature = float(self.model.logit_scale.detach().float().exp().item())
+        return combined, txt, temperature, (s_img, s_ctx, s_fuse, s_txt)
+
+    def forward(self, pixel_values, context_features=None, use_adapters_for_training=True):
+        combined, txt, temperature, _ = self._forward(pixel_values, context_features)
+        return class_scores(combined, txt, self._bank.protos_offsets, temperature)[0]
+
+    def predict_probs(self, pixel_values, context_features=None):
+        """model_v.py:345-353."""
+        self.eval()
+        combined, txt, temperature, _ = self._forward(pixel_values, context_features)
+        return class_scores(combined, txt, self._bank.protos_offsets, temperature)[1]
+
+    def get_trainable_parameters(self):
+        params = []
+        for ad in self._adapters():
+            params.extend(list(ad.parameters()))
+        return params
+
+    def train_step(self, pixel_values, labels, context_features, learning_rate):
+        """One iteration of main.py:66-86: logits -> CrossEntropy -> backward -> Adam (all three
+        adapters).  Labels are validated on the host first (no update on a bad batch)."""
+        lab = torch.as_tensor(labels).detach().to("cpu", torch.int64)
+        C = self.emotion_embedding_tensor.shape[0]
+        bad_lab = lab[(lab < 0) | (lab >= C)]
+        if bad_lab.numel():
+            raise IndexError(f"Target {int(bad_lab[0])} is out of bounds.")
+        combined, txt, temperature, (s_img, s_ctx, s_fuse, s_txt) = self._forward(pixel_values, context_features)
+        _, _, loss_rows, dscore, _ = class_scores(combined, txt, self._bank.protos_offsets, temperature, labels)
+        B, E = combined.shape
+        loss = torch.empty(1, dtype=torch.float32, device=combined.device)
+        call("clipmi_row_mean", T.K.stream(), P_(loss_rows), B, P_(loss))
+        dcomb, dtxt = torch.empty_like(combined), torch.empty_like(txt)
+        call("clipmi_class_ce_bwd", T.K.stream(), P_(dscore), P_(combined), P_(txt), B, C, E, float(temperature), None,
+             P_(dcomb), P_(dtxt))
+        for ad in self._adapters():
+            ad.grad.zero_()  # optimizer.zero_grad()
+        if s_fuse is not None:
+            dab = torch.empty_like(dcomb)
+            call("clipmi_fuse_avg_bwd", T.K.stream(), P_(dcomb), P_(s_fuse[0]), P_(s_fuse[1]), B, E, P_(dab))
+            self.visual_adapter.backward_(dab, s_img)
+            self.context_adapter.backward_(dab, s_ctx)
+        else:
+            self.visual_adapter.backward_(dcomb, s_img)
+        if s_txt is not None:
+            self.text_adapter.backward_(dtxt, s_txt)
+        for ad in self._adapters():
+            ad.adam_step(learning_rate)
+        return loss
+
+    def train_adapters(self, train_loader, num_epochs, learning_rate):
+        """main.py:55-100 (train_model): Adam over the adapters, CE on the logits, the emotion
+        embeddings refreshed after each epoch; returns the per-epoch mean losses."""
+        self.train()
+        history = []
+        for _ in range(num_epochs):
+            losses = []
+            for pixel_values, labels, _, context_features in train_loader:
+                losses.append(self.train_step(pixel_values, labels, context_features, learning_rate))
+            history.append(float(torch.cat(losses).mean().item()))
+            self.update_emotion_embeddings()
+        self.eval()
+        return history

@@ -11,10 +11,14 @@ Every text token is processed independently (queries only attend to the image to
 only the pooled token reaches the features (model_m.py:102), so the adapter runs on that row
 alone.  fp32 throughout (a few MFLOP per caption): the clipmi fp32 GEMM with fused
 bias / GELU / residual epilogues, native LayerNorm, row softmax and column-sum kernels.
-Dropout (p=0.1 in the reference's training mode) is not applied: outputs equal the
-reference in eval mode, which is what the parity tests pin.
+Dropout (p = 0.1, adapter/clip_adapter.py:84,96) runs in training mode (nn.Module.train()) on
+the attention probabilities (nn.MultiheadAttention's dropout) and on mlp.2's output, with masks
+from libclipmi's seeded counter generator (clipmi_dropout_mask; a seed replays its masks); in
+eval mode the outputs equal the reference's, which is what the parity tests pin.
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
@@ -27,6 +31,8 @@ from .modules import ArenaModule
 P_, call, F32 = T.P_, T.call, T.F32
 _lib.declare("clipmi_softmax_rows", [T.c_vp, T.c_vp, T.c_vp, T.c_int, T.c_int, T.c_float])
 _lib.declare("clipmi_softmax_rows_bwd", [T.c_vp, T.c_vp, T.c_vp, T.c_vp, T.c_int, T.c_int, T.c_float])
+_lib.declare("clipmi_dropout_mask", [T.c_vp, T.c_vp, T.c_i64, T.c_float, ctypes.c_uint64, ctypes.c_uint64])
+_lib.declare("clipmi_dropout_apply", [T.c_vp, T.c_vp, T.c_vp, T.c_i64, T.c_float, T.c_vp, T.c_vp])
 
 HEAD = 64
 
@@ -46,12 +52,21 @@ def shared_specs(text_in, image_in, hidden=512):
 class SharedAdapterParams(ArenaModule):
     """Parameters with SharedMHSAttentionAdapter's state-dict names, in one fp32 arena."""
 
-    def __init__(self, text_in, image_in, device, hidden=512, seed=0, prefix="shared_adapters.0"):
+    def __init__(self, text_in, image_in, device, hidden=512, seed=0, prefix="shared_adapters.0", dropout=0.1):
         super().__init__(shared_specs(text_in, image_in, hidden), device, shadow=False)
         self.text_in, self.image_in, self.hidden = text_in, image_in, hidden
         if hidden % HEAD:
             raise ValueError("hidden_size must be a multiple of 64 (8 heads of 64 in the reference)")
         self.load_numpy(synth.shared_adapter_state_dict(text_in, image_in, seed, prefix, hidden))
+        self.p = float(dropout)
+        self.drop_seed = (seed * 1000003 + sum(map(ord, prefix))) & (2 ** 63 - 1)
+        self.drop_offset = 0
+
+    def dropout_mask(self, n, device):
+        keep = torch.empty(n, dtype=torch.uint8, device=device)
+        call("clipmi_dropout_mask", K.stream(), P_(keep), n, self.p, self.drop_seed, self.drop_offset)
+        self.drop_offset += n
+        return keep
 
 
 def _ln(x, w, b, R, D):
@@ -105,11 +120,17 @@ class SharedAdapterFn(torch.autograd.Function):
         K.gemm(Nv, H, H, ln1, H, True, Win[2 * H:], H, True, v, H, bias=bin_[2 * H:], flags=E_B)
         P, o = f(nh, R, Nv), f(R, H)
         scale = HEAD ** -0.5
+        drop = mod.training and mod.p > 0
+        ds = 1.0 / (1.0 - mod.p) if drop else 1.0
+        keep_p = mod.dropout_mask(nh * R * Nv, dev).view(nh, R, Nv) if drop else None
+        Pd = f(nh, R, Nv) if drop else P  # dropped probabilities (nn.MultiheadAttention dropout)
         for h in range(nh):
             c = slice(h * HEAD, (h + 1) * HEAD)
             K.gemm(R, Nv, HEAD, q[:, c], H, True, k[:, c], H, True, P[h], Nv)
             call("clipmi_softmax_rows", K.stream(), P_(P[h]), P_(P[h]), R, Nv, scale)
-            K.gemm(R, HEAD, Nv, P[h], Nv, True, v[:, c], H, False, o[:, c], H)
+            if drop:
+                call("clipmi_dropout_apply", K.stream(), P_(P[h]), P_(keep_p[h]), R * Nv, ds, None, P_(Pd[h]))
+            K.gemm(R, HEAD, Nv, Pd[h], Nv, True, v[:, c], H, False, o[:, c], H)
         t2 = f(R, H)
         K.gemm(R, H, H, o, H, True, W("cross_attn.out_proj.weight"), H, True, t2, H,
                bias=W("cross_attn.out_proj.bias"), residual=ln2, ldr=H, flags=E_B | E_R)
@@ -117,17 +138,25 @@ class SharedAdapterFn(torch.autograd.Function):
         pre, act, y = f(R, 4 * H), f(R, 4 * H), f(R, H)
         K.gemm(R, 4 * H, H, ln3, H, True, W("mlp.0.weight"), H, True, act, 4 * H, bias=W("mlp.0.bias"), aux=pre,
                ldaux=4 * H, flags=E_B | _lib.EPI_GELU | _lib.EPI_STORE_PRE)
-        K.gemm(R, H, 4 * H, act, 4 * H, True, W("mlp.2.weight"), 4 * H, True, y, H, bias=W("mlp.2.bias"),
-               residual=t2, ldr=H, flags=E_B | E_R)
+        keep_m = None
+        if drop:  # mlp = Sequential(Linear, GELU, Linear, Dropout): y = t2 + dropout(mlp.2(.))
+            z = f(R, H)
+            K.gemm(R, H, 4 * H, act, 4 * H, True, W("mlp.2.weight"), 4 * H, True, z, H, bias=W("mlp.2.bias"),
+                   flags=E_B)
+            keep_m = mod.dropout_mask(R * H, dev)
+            call("clipmi_dropout_apply", K.stream(), P_(z), P_(keep_m), R * H, ds, P_(t2), P_(y))
+        else:
+            K.gemm(R, H, 4 * H, act, 4 * H, True, W("mlp.2.weight"), 4 * H, True, y, H, bias=W("mlp.2.bias"),
+                   residual=t2, ldr=H, flags=E_B | E_R)
         if need:
-            ctx.save = (x32, img, t, u, ln1, st1, ln2, st2, q, k, v, P, o, t2, ln3, st3, pre, act)
+            ctx.save = (x32, img, t, u, ln1, st1, ln2, st2, q, k, v, P, Pd, o, t2, ln3, st3, pre, act, keep_p, keep_m, ds)
             ctx.mod, ctx.shape, ctx.dt = mod, shp, dt
         return y.view(*shp[:-1], H).to(dt)
 
     @staticmethod
     def backward(ctx, dy):
         mod = ctx.mod
-        x32, img, t, u, ln1, st1, ln2, st2, q, k, v, P, o, t2, ln3, st3, pre, act = ctx.save
+        x32, img, t, u, ln1, st1, ln2, st2, q, k, v, P, Pd, o, t2, ln3, st3, pre, act, keep_p, keep_m, ds = ctx.save
         a = mod.arena
         R, Nv, H, nh = x32.shape[0], img.shape[0], mod.hidden, mod.hidden // HEAD
         Dt, Dv = mod.text_in, mod.image_in
@@ -141,12 +170,16 @@ class SharedAdapterFn(torch.autograd.Function):
         gp = lambda n: a.ptr(n, a.grad) if train else None  # noqa: E731
         BETA = _lib.EPI_BETA
         d = dy.reshape(R, H).to(torch.float32).contiguous()
+        dm = d  # gradient reaching mlp.2's output (through its dropout)
+        if keep_m is not None:
+            dm = f(R, H)
+            call("clipmi_dropout_apply", K.stream(), P_(d), P_(keep_m), R * H, ds, None, P_(dm))
         # MLP
         if train:
-            K.gemm(H, 4 * H, R, d, H, False, act, 4 * H, False, G("mlp.2.weight"), 4 * H, flags=BETA)
-            _colsum(d, R, H, gp("mlp.2.bias"))
+            K.gemm(H, 4 * H, R, dm, H, False, act, 4 * H, False, G("mlp.2.weight"), 4 * H, flags=BETA)
+            _colsum(dm, R, H, gp("mlp.2.bias"))
         dpre = f(R, 4 * H)
-        K.gemm(R, 4 * H, H, d, H, True, W("mlp.2.weight"), 4 * H, False, dpre, 4 * H, aux=pre, ldaux=4 * H,
+        K.gemm(R, 4 * H, H, dm, H, True, W("mlp.2.weight"), 4 * H, False, dpre, 4 * H, aux=pre, ldaux=4 * H,
                flags=_lib.EPI_DGELU)
         if train:
             K.gemm(4 * H, H, R, dpre, 4 * H, False, ln3, H, False, G("mlp.0.weight"), H, flags=BETA)
@@ -166,10 +199,12 @@ class SharedAdapterFn(torch.autograd.Function):
         for h in range(nh):
             c = slice(h * HEAD, (h + 1) * HEAD)
             K.gemm(R, Nv, HEAD, do[:, c], H, True, v[:, c], H, True, dP, Nv)
+            if keep_p is not None:  # through the probabilities' dropout
+                call("clipmi_dropout_apply", K.stream(), P_(dP), P_(keep_p[h]), R * Nv, ds, None, P_(dP))
             call("clipmi_softmax_rows_bwd", K.stream(), P_(P[h]), P_(dP), P_(dP), R, Nv, scale)  # dP -> dS
             K.gemm(R, HEAD, Nv, dP, Nv, True, k[:, c], H, False, dq[:, c], H)
             K.gemm(Nv, HEAD, R, dP, Nv, False, q[:, c], H, False, dk[:, c], H)
-            K.gemm(Nv, HEAD, R, P[h], Nv, False, do[:, c], H, False, dv[:, c], H)
+            K.gemm(Nv, HEAD, R, Pd[h], Nv, False, do[:, c], H, False, dv[:, c], H)
         Win = W("cross_attn.in_proj_weight")
         if train:
             gWin = G("cross_attn.in_proj_weight")

@@ -31,7 +31,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // out = z/|z|, rz = 1/|z|
 __global__ __launch_bounds__(HT) void fadapt_fwd_kernel(const float* x, int E, int A, const float* W1, const float* b1,
                                                        const float* W2, const float* b2, float alpha, int norm_in,
-                                                       float* xn, float* h, float* out, float* rz) {
+                                                       float* xn, float* h, float* out, float* rz,
+                                                       const uint8_t* keep, float keep_scale) {
   __shared__ float sx[MAXE];
   __shared__ float sh[MAXA];
   __shared__ float red[4];
@@ -55,7 +56,8 @@ __global__ __launch_bounds__(HT) void fadapt_fwd_kernel(const float* x, int E, i
     for (int e = lane; e < E; e += 64) acc = fmaf(W1[(int64_t)a * E + e], sx[e], acc);
     acc = wave_sum(acc) + b1[a];
     if (lane == 0) {
-      const float r = fmaxf(acc, 0.f);
+      float r = fmaxf(acc, 0.f);
+      if (keep) r *= keep[row * A + a] ? keep_scale : 0.f;  // nn.Dropout after the ReLU (model_v.py:26)
       sh[a] = r;
       h[row * A + a] = r;
     }
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(HT) void fadapt_fwd_kernel(const float* x, int E, i
 // per row: dy = alpha * (dout - out (out . dout)) / |z|;  dh = [h > 0] * W2^T dy
 __global__ __launch_bounds__(HT) void fadapt_bwd_rows_kernel(const float* dout, const float* out, const float* rz, int E,
                                                             int A, const float* h, const float* W2, float alpha,
-                                                            float* dy, float* dh) {
+                                                            float* dy, float* dh, float keep_scale) {
   __shared__ float sdy[MAXE];
   __shared__ float red[4];
   const int t = threadIdx.x;
@@ -106,7 +108,8 @@ __global__ __launch_bounds__(HT) void fadapt_bwd_rows_kernel(const float* dout, 
   for (int a = t; a < A; a += HT) {  // thread per unit: W2[e, a] reads coalesced across threads
     float acc = 0.f;
     for (int e = 0; e < E; ++e) acc = fmaf(W2[(int64_t)e * A + a], sdy[e], acc);
-    dh[row * A + a] = h[row * A + a] > 0.f ? acc : 0.f;
+    // h holds relu(.) * mask / (1 - p): h > 0 <=> kept and active
+    dh[row * A + a] = h[row * A + a] > 0.f ? acc * keep_scale : 0.f;
   }
 }
 
@@ -245,6 +248,56 @@ __global__ __launch_bounds__(HT) void softmax_rows_bwd_kernel(const float* y, co
   for (int j = lane; j < N; j += 64) dx[row * N + j] = scale * y[row * N + j] * (dy[row * N + j] - d);
 }
 
+// keep[i] = u(seed, offset + i) >= p, u uniform in [0, 1) from a counter hash (splitmix64): the
+// masks of nn.Dropout(p) (model_v.py:25, adapter/clip_adapter.py:84,96) reproducible by seed
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(HT) void dropout_mask_kernel(uint8_t* keep, int64_t n, float p, uint64_t seed,
+                                                         uint64_t offset) {
+  const int64_t i = (int64_t)blockIdx.x * HT + threadIdx.x;
+  if (i >= n) return;
+  const float u = (float)(splitmix64(seed * 0x632BE59BD9B4E019ull + offset + (uint64_t)i) >> 40) * (1.0f / 16777216.0f);
+  keep[i] = u >= p ? 1 : 0;
+}
+// y = x * keep * scale (+ res)
+__global__ __launch_bounds__(HT) void dropout_apply_kernel(const float* x, const uint8_t* keep, int64_t n, float scale,
+                                                          const float* res, float* y) {
+  const int64_t i = (int64_t)blockIdx.x * HT + threadIdx.x;
+  if (i >= n) return;
+  float v = keep[i] ? x[i] * scale : 0.f;
+  if (res) v += res[i];
+  y[i] = v;
+}
+// average fusion (model_v.py:310-315): u = (a + b) / 2, out = u / |u|, ru = 1 / |u|
+__global__ __launch_bounds__(HT) void fuse_avg_kernel(const float* a, const float* b, int E, float* out, float* ru) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  float ss = 0.f;
+  for (int e = threadIdx.x; e < E; e += HT) {
+    const float u = 0.5f * (a[row * E + e] + b[row * E + e]);
+    ss += u * u;
+  }
+  ss = block_sum(ss, red);
+  const float r = 1.f / sqrtf(ss);
+  for (int e = threadIdx.x; e < E; e += HT) out[row * E + e] = 0.5f * (a[row * E + e] + b[row * E + e]) * r;
+  if (threadIdx.x == 0) ru[row] = r;
+}
+// d a = d b = (dout - out (out . dout)) * ru / 2
+__global__ __launch_bounds__(HT) void fuse_avg_bwd_kernel(const float* dout, const float* out, const float* ru, int E,
+                                                         float* dab) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  float dot = 0.f;
+  for (int e = threadIdx.x; e < E; e += HT) dot += out[row * E + e] * dout[row * E + e];
+  dot = block_sum(dot, red);
+  const float r = 0.5f * ru[row];
+  for (int e = threadIdx.x; e < E; e += HT) dab[row * E + e] = (dout[row * E + e] - out[row * E + e] * dot) * r;
+}
+
 }  // namespace
 
 extern "C" int clipmi_softmax_rows(void* stream, const float* x, float* y, int R, int N, float scale) {
@@ -267,12 +320,13 @@ extern "C" int clipmi_softmax_rows_bwd(void* stream, const float* y, const float
 
 extern "C" int clipmi_feature_adapter_fwd(void* stream, const float* x, int B, int E, int A, const float* W1,
                                           const float* b1, const float* W2, const float* b2, float alpha, int norm_in,
-                                          float* xn, float* h, float* out, float* rz) {
+                                          float* xn, float* h, float* out, float* rz, const uint8_t* keep,
+                                          float keep_scale) {
   CLIPMI_REQUIRE(B >= 0 && E >= 1 && E <= MAXE && A >= 1 && A <= MAXA, "feature adapter: E <= 1024, A <= 256");
   CLIPMI_REQUIRE(x && W1 && b1 && W2 && b2 && xn && h && out && rz, "feature adapter: null pointer");
   if (B == 0) return CLIPMI_OK;
   hipLaunchKernelGGL(fadapt_fwd_kernel, dim3(B), dim3(HT), 0, (hipStream_t)stream, x, E, A, W1, b1, W2, b2, alpha,
-                     norm_in, xn, h, out, rz);
+                     norm_in, xn, h, out, rz, keep, keep_scale);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
@@ -283,14 +337,16 @@ extern "C" int clipmi_feature_adapter_bwd_ws(int B, int E, int A) {
 
 extern "C" int clipmi_feature_adapter_bwd(void* stream, const float* dout, const float* out, const float* rz,
                                           const float* xn, const float* h, int B, int E, int A, const float* W2,
-                                          float alpha, float* grads, void* workspace, int64_t workspace_bytes) {
+                                          float alpha, float* grads, void* workspace, int64_t workspace_bytes,
+                                          float keep_scale) {
   CLIPMI_REQUIRE(B >= 0 && E >= 1 && E <= MAXE && A >= 1 && A <= MAXA, "feature adapter: E <= 1024, A <= 256");
   CLIPMI_REQUIRE(workspace_bytes >= clipmi_feature_adapter_bwd_ws(B, E, A), "feature adapter: workspace too small");
   if (B == 0) return CLIPMI_OK;
   hipStream_t s = (hipStream_t)stream;
   float* dy = (float*)workspace;
   float* dh = dy + (int64_t)B * E;
-  hipLaunchKernelGGL(fadapt_bwd_rows_kernel, dim3(B), dim3(HT), 0, s, dout, out, rz, E, A, h, W2, alpha, dy, dh);
+  hipLaunchKernelGGL(fadapt_bwd_rows_kernel, dim3(B), dim3(HT), 0, s, dout, out, rz, E, A, h, W2, alpha, dy, dh,
+                     keep_scale);
   const int64_t n = 2 * (int64_t)A * E + A + E;
   hipLaunchKernelGGL(fadapt_wgrad_kernel, dim3((unsigned)((n + HT - 1) / HT)), dim3(HT), 0, s, xn, h, dy, dh, B, E, A,
                      grads);
@@ -323,6 +379,42 @@ extern "C" int clipmi_class_ce_bwd(void* stream, const float* dscore, const floa
   const int64_t n = (int64_t)(B + C) * E;
   hipLaunchKernelGGL(class_ce_bwd_kernel, dim3((unsigned)((n + HT - 1) / HT)), dim3(HT), 0, (hipStream_t)stream,
                      dscore, img, protos, B, C, E, scale, gscale, dimg, dprotos);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_dropout_mask(void* stream, uint8_t* keep, int64_t n, float p, uint64_t seed, uint64_t offset) {
+  CLIPMI_REQUIRE(n >= 0 && p >= 0.f && p < 1.f, "dropout: 0 <= p < 1");
+  if (n == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((n + HT - 1) / HT)), dim3(HT), 0, (hipStream_t)stream, keep,
+                     n, p, seed, offset);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_dropout_apply(void* stream, const float* x, const uint8_t* keep, int64_t n, float scale,
+                                    const float* res, float* y) {
+  CLIPMI_REQUIRE(n >= 0 && x && keep && y, "dropout apply: null pointer");
+  if (n == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(dropout_apply_kernel, dim3((unsigned)((n + HT - 1) / HT)), dim3(HT), 0, (hipStream_t)stream, x,
+                     keep, n, scale, res, y);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_fuse_avg(void* stream, const float* a, const float* b, int B, int E, float* out, float* ru) {
+  CLIPMI_REQUIRE(B >= 0 && E >= 1, "fuse_avg: bad shape");
+  if (B == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(fuse_avg_kernel, dim3(B), dim3(HT), 0, (hipStream_t)stream, a, b, E, out, ru);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_fuse_avg_bwd(void* stream, const float* dout, const float* out, const float* ru, int B, int E,
+                                   float* dab) {
+  CLIPMI_REQUIRE(B >= 0 && E >= 1, "fuse_avg: bad shape");
+  if (B == 0) return CLIPMI_OK;
+  hipLaunchKernelGGL(fuse_avg_bwd_kernel, dim3(B), dim3(HT), 0, (hipStream_t)stream, dout, out, ru, E, dab);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
