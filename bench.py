@@ -39,6 +39,7 @@ from clipmi import config as C  # noqa: E402
 
 METRIC = "image-text pairs/sec, ViT-B/16 contrastive step, 1/2/4/8 GPUs; MFMA % peak"
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/CU/clk (dense bf16, MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5033.2   # block-scaled f8f6f4 MFMA: 2x the bf16 rate (dense)
 
 
 def log(msg):
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: the frozen towers' GEMMs in MXFP8 (BASELINE config 5; needs --mode adapter)")
     ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES),
                     help="family reported as `roofline` (default: the one with the most measured time)")
     ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
@@ -85,6 +88,8 @@ FAMILIES = {
                           "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad", "gemm256_dgrad_dqgelu"],
     "gemm256_wgrad": ["gemm256_wgrad_splitk", "gemm256_wgrad"],
     "attention": ["attn_fwd", "attn_bwd"],
+    "gemm_fp8": ["gemm_fp8_fwd_bias", "gemm_fp8_fwd_bias_resid", "gemm_fp8_fwd_bias_qgelu",
+                 "gemm_fp8_fwd_bias_qgelu_q8", "gemm_fp8", "gemm_fp8_generic"],
 }
 # HBM traffic per launch of each family, from rocprofv3 --pmc passes (tools/traffic_pmc.sh); named
 # explicitly so the file read is the one committed for this build, not the newest on disk
@@ -122,7 +127,39 @@ def algorithmic_bytes(cfg, B, train):
     return {k: round(v) for k, v in out.items()}
 
 
-def cpu_baseline(cfg, B, steps):
+def cpu_baseline_adapter(cfg, B, steps, threads):
+    """Oracle adapter fine-tune step (frozen towers, configs 2/4/5) on the host: the towers' forward,
+    the adapters on the pooled rows (model_m.py:77-125), the contrastive loss and its backward into
+    the adapters (AdamW over ~1 M adapter parameters is negligible and left out)."""
+    from clipmi import synth
+    from oracle import clip_ref as R
+    torch.set_num_threads(threads)
+    p = {name: torch.randn(*shape) * std + mean for name, shape, std, mean in synth.clip_param_specs(cfg)}
+    p["logit_scale"] = torch.tensor(C.LN100)
+    t, v = cfg.text_config, cfg.vision_config
+    ta = R.to_torch(synth.adapter_state_dict(t.hidden_size, 256, 0, "text_adapter"), requires_grad=True)
+    va = R.to_torch(synth.adapter_state_dict(v.hidden_size, 256, 0, "vision_adapter"), requires_grad=True)
+    b = {k: torch.from_numpy(x) for k, x in synth.synthetic_batch(cfg, B, seed=1234).items()}
+    times = []
+    for it in range(steps + 1):
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            ht = R.text_tower(b["input_ids"], b["attention_mask"], p, cfg)[:, :1]
+            hv = R.vision_tower(b["pixel_values"], p, cfg)[:, :1]
+        tf = R.linear(R.adapter(ht, ta)[:, 0], p["text_projection.weight"])
+        imf = R.linear(R.adapter(hv, va)[:, 0], p["visual_projection.weight"])
+        R.contrastive(tf, imf, p["logit_scale"])["loss"].backward()
+        if it > 0:
+            times.append(time.perf_counter() - t0)
+        log(f"cpu baseline step {it}: {time.perf_counter() - t0:.2f} s")
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(B / med, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/clip_ref.py {cfg.name} adapter fine-tune step (frozen towers fwd + adapters fwd/bwd + "
+                      f"InfoNCE) fp32, B={B}, median of {steps} steps after 1 warm-up, torch CPU threads={threads}"}
+
+
+def cpu_baseline(cfg, B, steps, adapters=False):
     """Oracle (oracle/clip_ref.py) full fine-tune step on the host: fwd + bwd + AdamW."""
     from clipmi import synth
     from oracle import clip_ref as R
@@ -131,6 +168,8 @@ def cpu_baseline(cfg, B, steps):
     threads = len(os.sched_getaffinity(0))
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():
         threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    if adapters:
+        return cpu_baseline_adapter(cfg, B, steps, threads)
     torch.set_num_threads(threads)
     gen = torch.Generator().manual_seed(0)
     p = {}
@@ -190,10 +229,11 @@ def family_roofline(name, launches, cfg, B, train):
     tot_ms = sum(m for m, _ in launches)
     tot_fl = sum(f for _, f in launches)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
+    peak = PEAK_FP8_TFLOPS if name == "gemm_fp8" else PEAK_BF16_TFLOPS
     res = {"bound": "mfma", "kernel": name, "labels": FAMILIES[name], "launches": len(launches),
            "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
-           "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(ach / PEAK_BF16_TFLOPS, 4), "ms_per_step_caller_stream": None,
+           "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(ach / peak, 4), "ms_per_step_caller_stream": None,
            "traffic": None, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": None,
            "algorithmic_bytes": algorithmic_bytes(cfg, B, train).get(name)}
     tf = TRAFFIC_FILES.get(name)
@@ -233,8 +273,10 @@ def main():
 
     cfg = C.resolve(args.model)
     adapters = args.mode == "adapter"
+    if args.precision == "fp8" and not adapters:
+        raise SystemExit("--precision fp8 runs frozen towers: use --mode adapter")
     model = CLIPWithAdapters(args.model, use_text_adapter=adapters, use_vision_adapter=adapters,
-                             use_shared_adapters=False, freeze_clip=adapters, device=dev, precision="bf16",
+                             use_shared_adapters=False, freeze_clip=adapters, device=dev, precision=args.precision,
                              fast_init=True, process_group=group)
     params = [p for n, p in model.named_parameters() if p.requires_grad]
     opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas(), process_group=group)
@@ -327,7 +369,8 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp8 (MXFP8 e4m3 tower GEMMs; bf16 elsewhere)" if args.precision == "fp8" else "bf16",
         "data": f"synthetic: CLIP-normalised U[0,1) {cfg.vision_config.image_size}px pixels + BOS/random-id/EOS captions (77 tok, EOS pad), "
                 "random-init weights",
         "config": {"workload": f"{cfg.name} {'full fine-tune (adapters off)' if not adapters else 'adapter fine-tune'}"
@@ -335,7 +378,8 @@ def main():
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": cfg.vision_config.image_size,
                    "text_len": 77, "parallelism": f"dp{world}"},
-        "mfma_frac_step": round(value * step_flops_pair / (world * PEAK_BF16_TFLOPS * 1e12), 4),
+        "mfma_frac_step": round(value * step_flops_pair / (world * (PEAK_FP8_TFLOPS if args.precision == "fp8"
+                                                                      else PEAK_BF16_TFLOPS) * 1e12), 4),
         "step_tflops_per_gpu": round(value * step_flops_pair / world / 1e12, 1),
         "loss": round(float(loss.item()), 4),
         "roofline": roofs.get(main_fam) if main_fam else None,
@@ -343,7 +387,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, args.cpu_steps)
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, args.cpu_steps, adapters)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -22,7 +22,7 @@ extern "C" {
 #define CLIPMI_ERR_HIP -2       /* HIP runtime error -> RuntimeError */
 #define CLIPMI_ERR_UNSUPPORTED -3
 
-enum clipmi_dtype { CLIPMI_F32 = 0, CLIPMI_BF16 = 1 };
+enum clipmi_dtype { CLIPMI_F32 = 0, CLIPMI_BF16 = 1, CLIPMI_FP8 = 2 /* MXFP8: OCP e4m3 + E8M0 per 32 k */ };
 
 int clipmi_version(void);
 const char* clipmi_last_error(void);
@@ -55,6 +55,15 @@ typedef struct clipmi_gemm_desc {
   void* workspace; int64_t workspace_bytes;
   float* bias_grad;     /* wgrad only: bias_grad[m] += sum_k A(m,k) (fused Linear bias gradient, fp32) */
   int force_small_tile; /* 1: 128x128 register-staged kernel; >=2: 256-kernel schedule variant (bench) */
+  /* ab_dtype == CLIPMI_FP8 (BASELINE config 5, forward GEMMs of the frozen towers): A, B are OCP e4m3
+   * bytes, both k-major, K % 128 == 0; a_scale / b_scale are E8M0 bytes [rows][K/32] (OCP MX:
+   * element value = fp8 * 2^(scale - 127)); v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation,
+   * the bf16 epilogues.  c_dtype == CLIPMI_FP8 (flags bias and/or quick_gelu / gelu only, ldc == N,
+   * N % 32 == 0): C is written as MXFP8 too, e4m3 bytes [M, N] and E8M0 scales c_scale [M, N/32]
+   * (fc1 -> fc2 without a bf16 round trip). */
+  const uint8_t* a_scale;
+  const uint8_t* b_scale;
+  uint8_t* c_scale;
 } clipmi_gemm_desc;
 
 #define CLIPMI_EPI_BIAS 1
@@ -67,6 +76,11 @@ typedef struct clipmi_gemm_desc {
 #define CLIPMI_EPI_STORE_PRE 128
 
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
+/* MXFP8 quantisation of a [R, K] bf16/f32 matrix (row stride ldx elements) into OCP e4m3 bytes
+ * q [R, K] and E8M0 block scales [R, K/32]: per 32-element block the smallest power of two that
+ * brings the block's max |x| to <= 448, round-to-nearest-even. */
+int clipmi_quant_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, int64_t R, int K, uint8_t* q,
+                       uint8_t* scales);
 
 /* ---- LayerNorm ([HF] modeling_clip.py:357,359,605,642,559; adapter/clip_adapter.py:15,142) -------
  * y = LN(x [+ pos[row % period] (+ cls at row % period == 0)]) * w + b; mean/rstd saved (fp32).
@@ -75,6 +89,11 @@ int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
 int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy, const void* w,
                          const void* b, float* mean, float* rstd, int R, int D, float eps, const void* pos,
                          const void* cls, int period);
+/* The same LayerNorm (bf16 x, no embedding add) with its output written as MXFP8, quantised
+ * from the fp32 result as clipmi_quant_mxfp8 does: q8 [R, D] e4m3, s8 [R, D/32] E8M0.  Feeds the
+ * fp8 tower GEMMs (BASELINE config 5) without a bf16 round trip. D % 256 == 0, D <= 1024. */
+int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, uint8_t* q8, uint8_t* s8,
+                               const void* w, const void* b, float* mean, float* rstd, int R, int D, float eps);
 int64_t clipmi_layernorm_bwd_ws(int R, int D);
 /* dx = [dres +] LN'(dy); dw/db (fp32, may be NULL) accumulate when beta_wb. */
 int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
@@ -132,17 +151,23 @@ typedef struct clipmi_layer_act { /* saved activations; pre == NULL in inference
   void *x_in, *ln1, *qkv, *o, *h, *ln2, *pre, *act;
   float *mean1, *rstd1, *lse, *mean2, *rstd2;
 } clipmi_layer_act;
+typedef struct clipmi_layer_w8 { /* MXFP8 GEMM weights: e4m3 [out, in] + E8M0 scales [out, in/32] */
+  const void *qkv_w, *qkv_s, *out_w, *out_s, *fc1_w, *fc1_s, *fc2_w, *fc2_s;
+} clipmi_layer_w8;
 typedef struct clipmi_encoder_desc {
-  int dtype, B, N, D, F, H, L;
+  int dtype, B, N, D, F, H, L;  /* dtype CLIPMI_FP8: bf16 activations / LN / attention, MXFP8 GEMMs (forward only) */
   float eps;
   int causal;
   const int64_t* attention_mask;
-  const clipmi_layer_w* layers;  /* [L] */
+  const clipmi_layer_w* layers;  /* [L] (bf16 LN weights and biases also for CLIPMI_FP8) */
   clipmi_layer_grad* grads;      /* [L], backward only */
   clipmi_layer_act* act;         /* [L]; layer l writes its output to act[l+1].x_in (x_out for the last) */
   void* x_out;
   void* workspace;
   int64_t workspace_bytes;
+  const clipmi_layer_w8* layers8; /* [L], CLIPMI_FP8 only */
+  void* q8;                       /* CLIPMI_FP8: MXFP8 activation scratch, align256(R*D) + R*F bytes (R = B*N) */
+  void* s8;                       /* CLIPMI_FP8: its block scales, align256(R*D/32) + R*F/32 bytes */
 } clipmi_encoder_desc;
 int clipmi_encoder_fwd(void* stream, const clipmi_encoder_desc* d);
 int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d);

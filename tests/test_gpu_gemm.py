@@ -121,3 +121,116 @@ def test_wgrad_fused_bias_grad(T, Nout, Kin, split):
     torch.cuda.synchronize()
     assert (C - ref).abs().max().item() / ref.abs().max().item() < 1e-2
     assert (db - dref).abs().max().item() / dref.abs().max().item() < 1e-3
+
+
+# ------------------------------------------------------------------ MXFP8 (config 5)
+def _mx8_exact(R, K, seed):
+    """Small integers (exact in e4m3) with random E8M0 block scales 2^-2 .. 2^3."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    v = torch.randint(-8, 9, (R, K), generator=g).float()
+    s = torch.randint(125, 131, (R, K // 32), generator=g).to(torch.uint8)
+    q = v.to(torch.float8_e4m3fn).view(torch.uint8)
+    return kern.MX8(q.cuda(), s.cuda())
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 520, 256), (1024, 768, 1024), (77, 64, 640),
+                                   (256, 256, 384), (2304, 1280, 4096)])
+def test_gemm_fp8_block_scaled_exact(M, N, K):
+    """v_mfma_scale_f32_16x16x128_f8f6f4 GEMM: integer operands and power-of-two block scales make
+    every product and sum exact in fp32, so the result must equal the dequantised product exactly
+    (checks the fp8 fragment map and which lanes' scale bytes apply to which k-blocks)."""
+    A, B = _mx8_exact(M, K, 1), _mx8_exact(N, K, 2)
+    C = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    kern.gemm_fp8(M, N, K, A, B, C, N)
+    ref = A.dequant() @ B.dequant().t()
+    torch.cuda.synchronize()
+    assert torch.equal(C, ref), (C - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("flags", [0, _lib.EPI_BIAS, _lib.EPI_BIAS | _lib.EPI_RESID, _lib.EPI_BIAS | _lib.EPI_QGELU])
+def test_gemm_fp8_epilogues(flags):
+    M, N, K = 600, 384, 512
+    x = _mk((M, K), torch.bfloat16, 21)
+    w = _mk((N, K), torch.bfloat16, 22) * 0.05
+    A, B = kern.quant_mxfp8(x), kern.quant_mxfp8(w.contiguous())
+    bias = _mk((N,), torch.bfloat16, 23)
+    res = _mk((M, N), torch.bfloat16, 24)
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, residual=res, ldr=N, flags=flags)
+    acc = A.dequant() @ B.dequant().t()
+    ref, _ = _ref_epi(acc, flags, bias, None, res)
+    torch.cuda.synchronize()
+    assert (C.float() - ref).abs().max().item() / max(1.0, ref.abs().max().item()) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_quant_mxfp8_roundtrip(dtype):
+    """Per 32-element block: scale = the smallest power of two bringing max|x| to <= 448; every
+    element within e4m3's rounding (2^-4 relative, or the block's subnormal step)."""
+    R, K = 97, 1024
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = (torch.randn(R, K, generator=g) * torch.exp(torch.randn(R, K // 32, generator=g) * 3).repeat_interleave(32, 1))
+    x = x.to(dtype).cuda()
+    m = kern.quant_mxfp8(x)
+    d = m.dequant()
+    xf = x.float()
+    amax = xf.abs().view(R, K // 32, 32).amax(-1)
+    e = torch.ceil(torch.log2(amax / 448.0))
+    assert torch.equal(m.s.to(torch.int32) - 127, e.to(torch.int32))
+    step = torch.pow(2.0, e - 9).repeat_interleave(32, 1)
+    assert ((d - xf).abs() <= xf.abs() * 2.0 ** -4 + step).all()
+
+
+def _mx_close(m, ref, frac=0.99):
+    """MXFP8 m vs the fp32 values ref it should encode: the block scales equal ref's exact rule
+    (ceil(log2(amax / 448))) for nearly every block (an amax on a power-of-two boundary may round
+    either way after a different fp32 summation order) and every element within two e4m3 steps."""
+    R, K = ref.shape
+    amax = ref.abs().view(R, K // 32, 32).amax(-1)
+    e = torch.ceil(torch.log2(amax / 448.0)).clamp(-127, 127)
+    same = (m.s.to(torch.int32) - 127 == e.to(torch.int32)).float().mean().item()
+    assert same >= frac, same
+    d = m.dequant()
+    step = torch.pow(2.0, e - 9).repeat_interleave(32, 1)
+    err = (d - ref).abs() - (ref.abs() * 2.0 ** -3 + 2 * step)
+    assert (err <= 0).all(), err.max().item()
+
+
+def test_gemm_fp8_mxfp8_output():
+    """fc1's fused epilogue in the fp8 towers: bias + quick_gelu, written as MXFP8 [M, N] + scales."""
+    M, N, K = 600, 512, 512
+    x = _mk((M, K), torch.bfloat16, 31)
+    w = _mk((N, K), torch.bfloat16, 32) * 0.05
+    A, B = kern.quant_mxfp8(x), kern.quant_mxfp8(w.contiguous())
+    bias = _mk((N,), torch.bfloat16, 33)
+    C = kern.MX8(torch.empty(M, N, dtype=torch.uint8, device="cuda"),
+                 torch.empty(M, N // 32, dtype=torch.uint8, device="cuda"))
+    flags = _lib.EPI_BIAS | _lib.EPI_QGELU
+    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, flags=flags)
+    acc = A.dequant() @ B.dequant().t()
+    ref, _ = _ref_epi(acc, flags, bias, None, None)
+    torch.cuda.synchronize()
+    _mx_close(C, ref)
+
+
+def test_gemm_fp8_mxfp8_output_rejects_residual():
+    M, N, K = 256, 256, 128
+    A, B = _mx8_exact(M, K, 1), _mx8_exact(N, K, 2)
+    C = kern.MX8(torch.empty(M, N, dtype=torch.uint8, device="cuda"),
+                 torch.empty(M, N // 32, dtype=torch.uint8, device="cuda"))
+    res = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        kern.gemm_fp8(M, N, K, A, B, C, N, residual=res, ldr=N, flags=_lib.EPI_RESID)
+
+
+@pytest.mark.parametrize("R,D", [(1000, 1024), (77, 768), (4, 512)])
+def test_layernorm_mxfp8(R, D):
+    """clipmi_layernorm_fwd_mxfp8 = LayerNorm in fp32, quantised like clipmi_quant_mxfp8."""
+    x = _mk((R, D), torch.bfloat16, 41) * 3
+    w = (1 + 0.1 * _mk((D,), torch.bfloat16, 42)).to(torch.bfloat16)
+    b = (0.1 * _mk((D,), torch.bfloat16, 43)).to(torch.bfloat16)
+    m, mean, rstd = kern.layernorm_mxfp8(x, w, b, 1e-5)
+    ref = torch.nn.functional.layer_norm(x.float(), (D,), w.float(), b.float(), 1e-5)
+    torch.cuda.synchronize()
+    _mx_close(m, ref)
+    assert torch.allclose(mean, x.float().mean(1), atol=1e-4)

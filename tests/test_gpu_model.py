@@ -40,7 +40,9 @@ def make(preset, adapters, precision, freeze=True):
                                                    ("b32_noadapter", "B/32", 8, False),
                                                    ("b16", "B/16", 4, False),
                                                    # config 4's model: P=14 (patch K 588 -> 640), N=257
-                                                   ("l14", "L/14", 2, True)])
+                                                   ("l14", "L/14", 2, True),
+                                                   # config 5's model at 336 px: N = 577 (streamed attention)
+                                                   ("l14_336", "L/14@336", 2, True)])
 def test_forward_matches_reference(golden, precision, tag, preset, B, adapters):
     g = golden(f"forward_{tag}.npz")
     m = make(preset, adapters, precision)
@@ -392,3 +394,117 @@ def test_shared_adapters_training_dropout_matches_oracle_with_same_masks():
         a1 = m.get_text_features(b["input_ids"], b["attention_mask"])
         a2 = m.get_text_features(b["input_ids"], b["attention_mask"])
     assert torch.equal(a1, a2)  # no dropout in eval mode
+
+
+# MXFP8 towers (BASELINE config 5).  Stated tolerance: every GEMM input is rounded to e4m3 (3
+# mantissa bits, one power-of-two scale per 32 inputs), i.e. ~2-3 % per element, over 24 + 12
+# layers; the logits (100 x cosine) are bounded by FP8_LOGIT_TOL and the features' direction by a
+# cosine similarity with the reference's.
+FP8_LOGIT_TOL = 2.0
+FP8_FEATURE_COS = 0.99
+
+
+@pytest.mark.parametrize("tag,preset,B", [("l14_336", "L/14@336", 2), ("b32", "B/32", 8)])
+def test_fp8_towers_match_reference(golden, tag, preset, B):
+    g = golden(f"forward_{tag}.npz")
+    m = make(preset, True, "fp8")
+    with torch.no_grad():
+        out = m(**batch(m.config, B, g))
+        fb = make(preset, True, "bf16")(**batch(m.config, B, g))
+    torch.cuda.synchronize()
+    lt = out["logits_per_text"].cpu().numpy()
+    err = float(np.abs(lt - g["logits_per_text"]).max())
+    err16 = float(np.abs(fb["logits_per_text"].cpu().numpy() - g["logits_per_text"]).max())
+
+    def cos(a, b):
+        a, b = a.astype(np.float64), b.astype(np.float64)
+        return float(((a * b).sum(-1) / (np.linalg.norm(a, axis=-1) * np.linalg.norm(b, axis=-1))).min())
+    ci = cos(out["image_features"].cpu().numpy(), g["image_features"])
+    ct = cos(out["text_features"].cpu().numpy(), g["text_features"])
+    print(f"\n[{tag} fp8] max|dlogit| {err:.4f} (bf16 {err16:.4f}); min feature cosine image {ci:.5f} text {ct:.5f}")
+    assert err < FP8_LOGIT_TOL, err
+    assert ci > FP8_FEATURE_COS and ct > FP8_FEATURE_COS, (ci, ct)
+
+
+def test_fp8_rejects_training_towers():
+    with pytest.raises(ValueError, match="frozen"):
+        CLIPWithAdapters("tiny", freeze_clip=False, device="cuda", precision="fp8")
+
+
+# Tensors whose gradient is summed with fp32 atomics (order varies between runs, so equal only to
+# rounding): the token-embedding scatter (wave-aggregated atomics per id chunk) and the Linear bias
+# gradients fused into split-K weight-gradient GEMMs (one atomicAdd per k-slab).
+_ATOMIC_GRADS = ("token_embedding.weight", ".bias")
+
+
+@pytest.mark.parametrize("freeze", [True, False])
+def test_deterministic_replay(freeze):
+    """SURVEY §5 race check: the same step twice on the same inputs.  Logits and loss must be
+    bitwise equal, and so must every gradient not accumulated by atomics (a racy kernel shows up
+    as a bitwise difference here); the atomic-summed ones within fp32 rounding."""
+    runs = []
+    for _ in range(2):
+        m = CLIPWithAdapters("B/32", freeze_clip=freeze, use_shared_adapters=False, device="cuda",
+                             precision="bf16", init_seed=3)
+        b = batch(m.config, 64)
+        out = m(**b, return_loss=True)
+        out["loss"].backward()
+        torch.cuda.synchronize()
+        runs.append((out["logits_per_image"].detach().clone(), out["loss"].detach().clone(),
+                     {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
+        del m, out
+    (l0, s0, g0), (l1, s1, g1) = runs
+    assert torch.equal(l0, l1) and torch.equal(s0, s1)
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    racy = []
+    for n in g0:
+        if torch.equal(g0[n], g1[n]):
+            continue
+        d = (g0[n] - g1[n]).abs().max().item() / max(g0[n].abs().max().item(), 1e-30)
+        if any(k in n for k in _ATOMIC_GRADS) and d < 1e-5:
+            continue
+        racy.append((n, d))
+    print(f"\n[replay freeze={freeze}] {len(g0)} gradients, not bitwise equal beyond atomics: {racy[:8]}")
+    assert not racy, racy
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 0.15)])
+def test_load_reference_checkpoint(golden, tmp_path, precision, tol):
+    """The reference's test_checkpoints/test_adapter.pt (tensors in tests/golden, written back here
+    in its {"text_adapter": sd, "vision_adapter": sd} format) through load_adapter_weights; the
+    forward must match the reference model that loaded the original file."""
+    g = golden("checkpoint_test_adapter.npz")
+    ck = {top: {k.split("/", 1)[1]: torch.from_numpy(g[k].copy()) for k in g.files if k.startswith(top + "/")}
+          for top in ("text_adapter", "vision_adapter")}
+    path = tmp_path / "test_adapter.pt"
+    torch.save(ck, path)
+    m = CLIPWithAdapters("B/32", use_shared_adapters=False, device="cuda", precision=precision)
+    m.load_adapter_weights(str(path))
+    for top, mod in (("text_adapter", m.text_adapter), ("vision_adapter", m.vision_adapter)):
+        sd = mod.state_dict()
+        for k, v in ck[top].items():
+            assert torch.equal(sd[k].float().cpu(), v), (top, k)
+    with torch.no_grad():
+        out = m(**batch(m.config, 2, g), return_loss=True)
+    got = out["logits_per_text"].float().cpu().numpy()
+    err = float(np.abs(got - g["logits_per_text"]).max())
+    print(f"\n[reference checkpoint {precision}] max|dlogit| {err:.3g}")
+    assert err < tol
+
+
+def test_enhanced_adapter_main_checkpoint_roundtrip(tmp_path):
+    """main.py:186-193's EnhancedCLIPAdapter checkpoint schema: save -> load into a fresh head."""
+    from clipmi.heads import EnhancedCLIPAdapter
+    a = EnhancedCLIPAdapter("tiny", device="cuda", seed=1)
+    b = EnhancedCLIPAdapter(a.model, device="cuda", seed=2)
+    path = tmp_path / "enhanced_adapters_weights.pth"
+    a.save_adapter_weights(str(path))
+    sd = torch.load(path, weights_only=True)
+    assert set(sd) == {"visual_adapter_state_dict", "text_adapter_state_dict", "context_adapter_state_dict"}
+    assert set(sd["visual_adapter_state_dict"]) == {"fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"}
+    b.load_adapter_weights(str(path))
+    for name in ("visual_adapter", "text_adapter", "context_adapter"):
+        for k, v in getattr(a, name).state_dict().items():
+            assert torch.equal(getattr(b, name).state_dict()[k], v)
+    with pytest.raises(FileNotFoundError):
+        b.load_adapter_weights(str(tmp_path / "missing.pth"))

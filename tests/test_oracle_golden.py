@@ -41,6 +41,7 @@ def batch(cfg, B, g):
     ("b32_noadapter", "B/32", 8, False),
     ("b16", "B/16", 4, False),
     ("l14", "L/14", 2, True),
+    ("l14_336", "L/14@336", 2, True),  # BASELINE config 5's model: N = 577 vision tokens
 ])
 def test_forward_matches_reference(golden, tag, preset, B, adapters):
     g = golden(f"forward_{tag}.npz")
@@ -253,3 +254,19 @@ def test_b32_adapter_b256_forward(golden):
         out = R.clip_with_adapters_forward(batch(cfg, 256, g), p, cfg, ta, va)
     np.testing.assert_allclose(out["logits_per_text"].numpy(), g["logits_per_text"], atol=1e-4)
     np.testing.assert_allclose(out["loss"].item(), g["loss"], atol=1e-5)
+
+
+def test_reference_checkpoint_forward(golden):
+    """The reference's own test_checkpoints/test_adapter.pt (its tensors, converted into the
+    fixture by tools/gen_goldens.py with the safe loader) loaded into B/32 adapters: the oracle's
+    forward equals the reference model's after model_m.load_adapter_weights."""
+    g = golden("checkpoint_test_adapter.npz")
+    cfg = C.resolve("B/32")
+    p, _, _ = model_params(cfg, False)
+    ta = {k.split("/", 1)[1]: torch.from_numpy(g[k]) for k in g.files if k.startswith("text_adapter/")}
+    va = {k.split("/", 1)[1]: torch.from_numpy(g[k]) for k in g.files if k.startswith("vision_adapter/")}
+    assert len(ta) == 6 and len(va) == 6
+    with torch.no_grad():
+        out = R.clip_with_adapters_forward(batch(cfg, 2, g), p, cfg, ta, va)
+    for k in ("logits_per_text", "text_features", "image_features"):
+        np.testing.assert_allclose(out[k].numpy(), g[k], atol=2e-5, rtol=1e-4, err_msg=k)

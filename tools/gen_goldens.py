@@ -223,6 +223,12 @@ def gen_shared_unfrozen():
     save("shared_adapters_unfrozen.npz", **out)
 
 
+def gen_l14_336():
+    """BASELINE config 5's model: ViT-L/14 at 336 px (N = 577 vision tokens, [HF] modeling_clip.py:202-218)
+    + adapters, frozen towers, B = 2: forward (features, logits, loss)."""
+    gen_forward("L/14@336", 2, "l14_336", adapters=True, grads=False)
+
+
 def gen_l14():
     """Config 4's model: ViT-L/14 (P=14 -> patch K=588, N=257 tokens) + adapters, frozen towers, with the
     adapter gradients (the trainable set of the adapter fine-tune)."""
@@ -392,6 +398,26 @@ def gen_checkpoint_schema():
     with open(os.path.join(OUT, "test_adapter_schema.json"), "w") as f:
         json.dump(schema, f, indent=1, sort_keys=True)
     print("schema", schema)
+
+
+def gen_checkpoint_fixture():
+    """The reference's own adapter checkpoint (test_checkpoints/test_adapter.pt, read with the safe
+    loader) as tensors, plus the reference model's forward with it loaded through
+    model_m.load_adapter_weights (B/32 towers from clipmi.synth, B=2): pins loading the real file."""
+    path = os.path.join(REF, "test_checkpoints", "test_adapter.pt")
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    out = {f"{top}/{k}": v.numpy() for top, sub in sd.items() for k, v in sub.items()}
+    cfg = C.resolve("B/32")
+    ref = build_reference_model(cfg)
+    ref.load_adapter_weights(path)
+    ref.eval()
+    b_np, b = batch_tensors(cfg, 2)
+    out["input_digest"] = np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"]))
+    with torch.no_grad():
+        res = ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=b["pixel_values"])
+    for k, v in res.items():
+        out[k] = v.detach().numpy()
+    save("checkpoint_test_adapter.npz", **out)
 
 
 def gen_quirks():

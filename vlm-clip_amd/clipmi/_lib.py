@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libclipmi.so")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 EPI_BIAS, EPI_QGELU, EPI_GELU, EPI_RESID = 1, 2, 4, 8
 EPI_DQGELU, EPI_DGELU, EPI_BETA, EPI_STORE_PRE = 16, 32, 64, 128
 
@@ -31,7 +31,8 @@ class GemmDesc(ctypes.Structure):
                 ("ab_dtype", ctypes.c_int), ("c_dtype", ctypes.c_int), ("bias_dtype", ctypes.c_int),
                 ("split_k", ctypes.c_int),
                 ("workspace", c_vp), ("workspace_bytes", c_i64),
-                ("bias_grad", c_vp), ("force_small_tile", ctypes.c_int)]
+                ("bias_grad", c_vp), ("force_small_tile", ctypes.c_int),
+                ("a_scale", c_vp), ("b_scale", c_vp), ("c_scale", c_vp)]
 
 
 class ClipmiError(RuntimeError):

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 from torch import nn
@@ -110,6 +111,15 @@ class FeatureAdapter(nn.Module):
                 if tuple(src.shape) != tuple(dst.shape):
                     raise ValueError(f"{k}: shape {tuple(src.shape)} != {tuple(dst.shape)}")
                 dst.copy_(src)
+
+    def state_dict(self, *args, **kwargs):
+        """nn.Linear key names of model_t / model_v adapters (fc1.weight, fc1.bias, fc2.weight, fc2.bias)."""
+        return self.state_dict_()
+
+    def load_state_dict(self, state_dict, strict=True):
+        if strict and set(state_dict) != {"fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"}:
+            raise RuntimeError(f"Error(s) in loading state_dict for {type(self).__name__}: keys {sorted(state_dict)}")
+        self.load_state_dict_(state_dict)
 
     def parameters(self, recurse=True):  # model_t passes these to optim.Adam
         return iter([self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias])
@@ -392,6 +402,22 @@ class EnhancedCLIPAdapter(nn.Module):
 
     def _adapters(self):
         return (self.visual_adapter, self.text_adapter, self.context_adapter)
+
+    _CKPT_KEYS = (("visual_adapter_state_dict", "visual_adapter"), ("text_adapter_state_dict", "text_adapter"),
+                  ("context_adapter_state_dict", "context_adapter"))
+
+    def save_adapter_weights(self, path):
+        """main.py:186-193's checkpoint: {visual,text,context}_adapter_state_dict -> nn.Linear state dicts."""
+        torch.save({k: getattr(self, a).state_dict() for k, a in self._CKPT_KEYS}, path)
+
+    def load_adapter_weights(self, path):
+        """Reads main.py:186-193's checkpoint (safe loader); a missing file raises FileNotFoundError and a
+        missing adapter key KeyError, as indexing the reference's dict would."""
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"No adapter weights found at {path}")
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        for k, a in self._CKPT_KEYS:
+            getattr(self, a).load_state_dict(sd[k])
 
     def encode_emotion_descriptions(self, emotions=None):
         """model_v.py:198-240: per emotion the mean of its normalised description features, then

@@ -10,7 +10,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import BF16, F32, GemmDesc
+from ._lib import BF16, F32, FP8, GemmDesc
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -84,3 +84,76 @@ def linear(x, w, bias=None, *, act=None, residual=None, out=None, pre_out=None):
          residual=residual.reshape(-1, N) if residual is not None else None, ldr=N,
          aux=pre_out, ldaux=N, flags=flags)
     return out.view(*x.shape[:-1], N)
+
+
+_lib.declare("clipmi_quant_mxfp8", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p])
+_lib.declare("clipmi_layernorm_fwd_mxfp8", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_float])
+
+
+class MX8:
+    """An MXFP8 matrix: OCP e4m3 bytes q [R, K] + E8M0 block scales s [R, K/32] (uint8)."""
+
+    def __init__(self, q, s):
+        self.q, self.s = q, s
+
+    @property
+    def shape(self):
+        return tuple(self.q.shape)
+
+    def dequant(self):
+        """fp32 values (for tests): fp8 * 2^(scale - 127)."""
+        v = self.q.view(torch.float8_e4m3fn).float()
+        e = self.s.to(torch.int32) - 127
+        return v * torch.pow(2.0, e.float()).repeat_interleave(32, dim=1)
+
+
+def quant_mxfp8(x, out=None):
+    """x [R, K] bf16/fp32 (K % 32 == 0) -> MX8 (clipmi_quant_mxfp8)."""
+    _on_gpu(x)
+    R, Kd = x.shape
+    if out is None:
+        out = MX8(torch.empty(R, Kd, dtype=torch.uint8, device=x.device),
+                  torch.empty(R, Kd // 32, dtype=torch.uint8, device=x.device))
+    _lib.check(_lib.lib().clipmi_quant_mxfp8(stream(), dt(x), x.data_ptr(), x.stride(0), R, Kd, out.q.data_ptr(),
+                                             out.s.data_ptr()), "clipmi_quant_mxfp8")
+    return out
+
+
+def layernorm_mxfp8(x, w, b, eps=1e-5):
+    """LayerNorm of x [R, D] (bf16) written as MXFP8 (clipmi_layernorm_fwd_mxfp8) -> (MX8, mean, rstd)."""
+    _on_gpu(x, w, b)
+    R, D = x.shape
+    out = MX8(torch.empty(R, D, dtype=torch.uint8, device=x.device),
+              torch.empty(R, D // 32, dtype=torch.uint8, device=x.device))
+    mean = torch.empty(R, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().clipmi_layernorm_fwd_mxfp8(stream(), dt(x), x.data_ptr(), x.stride(0), out.q.data_ptr(),
+                                                     out.s.data_ptr(), w.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                                     rstd.data_ptr(), R, D, eps), "clipmi_layernorm_fwd_mxfp8")
+    return out, mean, rstd
+
+
+def gemm_fp8(M, N, K, A, B, C, ldc, *, bias=None, residual=None, ldr=0, alpha=1.0, flags=0):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)) with A [M, K], B [N, K] MXFP8 (MX8).  C is a
+    tensor (bf16 / fp32) or an MX8 [M, N] (MXFP8 output: flags bias / activation only)."""
+    q8o = isinstance(C, MX8)
+    _on_gpu(A.q, B.q, C.q if q8o else C, bias, residual)
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = A.q.data_ptr(), A.q.stride(0), 1
+    d.B, d.ldb, d.b_kmajor = B.q.data_ptr(), B.q.stride(0), 1
+    d.a_scale, d.b_scale = A.s.data_ptr(), B.s.data_ptr()
+    d.C, d.ldc = (C.q if q8o else C).data_ptr(), ldc
+    d.c_scale = C.s.data_ptr() if q8o else None
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.residual, d.ldr = (residual.data_ptr() if residual is not None else None), ldr
+    d.alpha, d.flags = alpha, flags
+    d.ab_dtype, d.c_dtype = FP8, (FP8 if q8o else dt(C))
+    d.bias_dtype = dt(bias) if bias is not None else F32
+    d.split_k = 1
+    _lib.check(_lib.lib().clipmi_gemm(stream(), ctypes.byref(d)), "clipmi_gemm")
+    return C

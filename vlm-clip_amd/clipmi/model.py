@@ -5,7 +5,8 @@ checkpoint format and error types as the reference; the compute runs on libclipm
 (``clipmi.towers``).  Extensions, all keyword-only:
 
   device       where the fp32 parameter arenas live (default: cuda if available)
-  precision    "bf16" (MFMA path, default) or "fp32" (exact-f32 parity mode)
+  precision    "bf16" (MFMA path, default), "fp32" (exact-f32 parity mode) or "fp8" (frozen towers
+               with MXFP8 GEMMs, BASELINE config 5; adapters and the loss stay bf16 / fp32)
   pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
                (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
   init_seed    seed of the deterministic random init used when no weights file exists
@@ -35,6 +36,7 @@ class _Runtime:
         self.train_tower = False
         self.bad_flag = torch.zeros(1, dtype=torch.int32, device=self.arena.device)
         self.grad_hook = None  # data-parallel gradient-ready hook (CLIPWithAdapters.set_grad_hook)
+        self.fp8 = False  # precision="fp8": the frozen towers' GEMMs in MXFP8 (BASELINE config 5)
 
 
 def _anchor(module: nn.Module):
@@ -77,8 +79,10 @@ class CLIPWithAdapters(nn.Module):
         super().__init__()
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
-        if precision not in ("bf16", "fp32"):
-            raise ValueError("precision must be 'bf16' or 'fp32'")
+        if precision not in ("bf16", "fp32", "fp8"):
+            raise ValueError("precision must be 'bf16', 'fp32' or 'fp8'")
+        if precision == "fp8" and not freeze_clip:
+            raise ValueError("precision='fp8' runs the frozen towers only (MXFP8 forward GEMMs); use freeze_clip=True")
         if pooling not in ("first", "eos"):
             raise ValueError("pooling must be 'first' or 'eos'")
         cfg = C.resolve(clip_model_name)
@@ -86,8 +90,8 @@ class CLIPWithAdapters(nn.Module):
         self.precision = precision
         self.pooling = pooling
         self.process_group = process_group
-        dtype = torch.bfloat16 if precision == "bf16" else torch.float32
-        shadow = precision == "bf16"
+        dtype = torch.float32 if precision == "fp32" else torch.bfloat16
+        shadow = precision != "fp32"
         # model_m.py:29-30 — CLIPModel.from_pretrained / CLIPProcessor.from_pretrained
         self.clip = CLIPParams(cfg, device, shadow)
         self.clip.text_model.config = cfg.text_config
@@ -118,6 +122,7 @@ class CLIPWithAdapters(nn.Module):
                                                                       seed=init_seed, prefix=f"shared_adapters.{i}")
                                                   for i in range(shared_adapter_layers)])
         self._rt = _Runtime(self.clip, dtype)
+        self._rt.fp8 = precision == "fp8"
         if freeze_clip:
             self._freeze_clip_parameters()
 
@@ -175,7 +180,10 @@ class CLIPWithAdapters(nn.Module):
 
     # ------------------------------------------------------------------ features
     def _tower_training(self):
-        return torch.is_grad_enabled() and self.clip.arena.any_requires_grad()
+        train = torch.is_grad_enabled() and self.clip.arena.any_requires_grad()
+        if train and self._rt.fp8:
+            raise NotImplementedError("precision='fp8' towers are forward-only; freeze the CLIP parameters")
+        return train
 
     def _adapter_needs_grad(self, mod, x):
         return torch.is_grad_enabled() and (mod.arena.any_requires_grad() or x.requires_grad)

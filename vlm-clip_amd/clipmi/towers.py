@@ -44,12 +44,19 @@ class LayerAct(ctypes.Structure):
     _fields_ = [(n, c_vp) for n in A_FIELDS]
 
 
+W8_FIELDS = ["qkv_w", "qkv_s", "out_w", "out_s", "fc1_w", "fc1_s", "fc2_w", "fc2_s"]
+
+
+class LayerW8(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in W8_FIELDS]
+
+
 class EncoderDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("B", c_int), ("N", c_int), ("D", c_int), ("F", c_int), ("H", c_int),
                 ("L", c_int), ("eps", c_float), ("causal", c_int), ("attention_mask", c_vp),
                 ("layers", ctypes.POINTER(LayerW)), ("grads", ctypes.POINTER(LayerG)),
                 ("act", ctypes.POINTER(LayerAct)), ("x_out", c_vp), ("workspace", c_vp),
-                ("workspace_bytes", c_i64)]
+                ("workspace_bytes", c_i64), ("layers8", ctypes.POINTER(LayerW8)), ("q8", c_vp), ("s8", c_vp)]
 
 
 P = ctypes.POINTER
@@ -195,10 +202,43 @@ class Encoder:
                 acts[i].pre = None
         return buf, acts
 
-    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None):
+    def weights8(self):
+        """MXFP8 copies of the four GEMM weights of every layer (BASELINE config 5), quantised from
+        the fp32 masters (clipmi_quant_mxfp8: e4m3 + one E8M0 scale per 32 inputs of an output row),
+        rebuilt when the masters change."""
+        a = self.arena
+        key = ("w8", a.data.data_ptr(), a.data._version)
+        hit = self._wcache.get("w8")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        L = self.t.num_hidden_layers
+        tab = (LayerW8 * L)()
+        keep = []
+        for i in range(L):
+            n = self.names(i)
+            D = self.t.hidden_size
+            q0 = a.offsets[n["qkv_w"]][0]  # q/k/v weights are adjacent: the fused [3D, D] matrix
+            for f, src in (("qkv", a.data[q0:q0 + 3 * D * D].view(3 * D, D)),
+                           ("out", a.view(n["out_w"])), ("fc1", a.view(n["fc1_w"])), ("fc2", a.view(n["fc2_w"]))):
+                m = K.quant_mxfp8(src.contiguous())
+                keep.append(m)
+                setattr(tab[i], f + "_w", m.q.data_ptr())
+                setattr(tab[i], f + "_s", m.s.data_ptr())
+        self._wcache["w8"] = (key, tab, keep)
+        return tab
+
+    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None, fp8=False):
         t = self.t
         d = EncoderDesc()
         d.dtype, d.B, d.N, d.D, d.F = dcode(dtype), B, N, t.hidden_size, t.intermediate_size
+        if fp8:  # bf16 activations, MXFP8 GEMMs (forward only)
+            d.dtype = _lib.FP8
+            d.layers8 = self.weights8()
+            R, Dh, F = B * N, t.hidden_size, t.intermediate_size
+            q8 = torch.empty(R * (Dh + F) + 512, dtype=torch.uint8, device=self.arena.device)
+            s8 = torch.empty(R * (Dh + F) // 32 + 512, dtype=torch.uint8, device=self.arena.device)
+            self._scratch8 = (q8, s8)  # alive until the next call; stream order covers reuse
+            d.q8, d.s8 = q8.data_ptr(), s8.data_ptr()
         d.H, d.L, d.eps, d.causal = t.num_attention_heads, t.num_hidden_layers, t.layer_norm_eps, int(self.causal)
         d.attention_mask = P_(mask)
         d.layers = self.weights(wbuf)
@@ -300,7 +340,7 @@ class VisionTowerFn(torch.autograd.Function):
              arena.ptr("vision_model.embeddings.position_embedding.weight", wbuf),
              arena.ptr("vision_model.embeddings.class_embedding", wbuf), N)
         out = torch.empty(B, N, D, dtype=dtype, device=dev)
-        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None)
+        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None, fp8=rt.fp8 and not train)
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
         if train:
             ctx.rt, ctx.B, ctx.buf, ctx.acts, ctx.X, ctx.h0, ctx.stats0 = rt, B, buf, acts, X, h0, stats0
@@ -384,7 +424,7 @@ class TextTowerFn(torch.autograd.Function):
              arena.ptr("text_model.embeddings.position_embedding.weight", wbuf), acts[0].x_in, R, S, D, t.vocab_size,
              P_(bad))
         xL = torch.empty(R, D, dtype=dtype, device=dev)
-        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask)
+        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask, fp8=rt.fp8 and not train)
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
         out = torch.empty(B, S, D, dtype=dtype, device=dev)
         stats = torch.empty(2, R, dtype=torch.float32, device=dev)

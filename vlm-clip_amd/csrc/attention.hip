@@ -993,7 +993,7 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
     fa_stage(slot + FA_TILE / 2, base + 2 * D, ld, kt * FA_KT, N, FA_KT / 8, wave, lane);
   };
   for (int kt = 0; kt < FA_S - 1 && kt < nkt; ++kt) issue(kt);
-  fa_vmcnt(4 * min(FA_S - 1, nkt));  // the Q chunk landed (this wave's part)
+  fa_vmcnt(4 * (min(FA_S - 1, nkt) - 1));  // the Q chunk and K/V tile 0 landed (this wave's part)
   fa_barrier();
   // this wave's query blocks: w + FA_W * u (interleaved: balanced under causal masking)
   bf16x8 qf[QPW][2];
@@ -1110,11 +1110,7 @@ void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s) {
   constexpr int QC = FA_W * QPW * 16;
   const int nkt = (p.N + FA_KT - 1) / FA_KT;
   const size_t lds = (size_t)QC * 128 + FA_S * FA_TILE + (M ? (size_t)nkt * FA_KT * 4 : 0);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_fa<QPW, M>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  (void)lds_optin((const void*)attn_fwd_fa<QPW, M>, 160 * 1024);
   const int nqc = (p.N + QC - 1) / QC;
   hipLaunchKernelGGL((attn_fwd_fa<QPW, M>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc);
 }
@@ -1311,11 +1307,7 @@ template <int NKT, bool M>
 void launch_fwd_pf(const AttnP& p, int causal, hipStream_t s) {
   constexpr int NPAD = NKT * 16;
   constexpr size_t lds = 4 * (size_t)NPAD * 128 + 2 * NPAD * sizeof(int);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_pf<NKT, M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
+  (void)lds_optin((const void*)attn_fwd_pf<NKT, M>, (int)lds);
   const int nitems = p.B * p.H;
   const int per_cu = (int)std::min<size_t>(2, (160 * 1024) / lds);
   const int grid = std::min(nitems, 256 * per_cu);
@@ -1344,11 +1336,7 @@ template <bool C, int NW>
 void launch_bwd_pf(const AttnP& p, hipStream_t s) {
   const int npad = (p.N + 31) & ~31;
   const size_t lds = 5 * (size_t)npad * 128 + 6 * (size_t)npad * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_pf<C, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  (void)lds_optin((const void*)attn_bwd_pf<C, NW>, 160 * 1024);
   const int nitems = p.B * p.H;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
   const int grid = std::min(nitems, 256 * per_cu);
@@ -1393,11 +1381,7 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
   } else {
     AttnF p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, causal, 0.125f};
     size_t lds = (size_t)F32_CH * 64 * 4 * 2 + (size_t)N * 4;
-    static bool attr = false;
-    if (!attr) {
-      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_fwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
+    CLIPMI_HIP(lds_optin((const void*)attn_fwd_f32, 160 * 1024));
     hipLaunchKernelGGL(attn_fwd_f32, dim3(B * H), dim3(1024), lds, s, p);
   }
   CLIPMI_CHECK_LAUNCH();
@@ -1415,24 +1399,16 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
     AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
     const int npad = (N + 31) & ~31;
     size_t lds = (size_t)npad * 128 * 2 + (size_t)npad * 12;
-    static bool attr = false;
-    if (!attr) {
-      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_mfma<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
+    CLIPMI_HIP(lds_optin((const void*)attn_bwd_mfma<true>, 160 * 1024));
+    CLIPMI_HIP(lds_optin((const void*)attn_bwd_mfma<false>, 160 * 1024));
     const double flops = 10.0 * B * H * (double)N * npad * 64;
     ProfScope ps(s, nullptr, flops);
     if (5 * (size_t)npad * 128 + 6 * (size_t)npad * 4 <= 160 * 1024) {  // N <= 224: prefetching kernel
       CLIPMI_TRY(bwd_pf_dispatch(p, causal, s));
     } else if (N > ATTN_MAX_N) {  // streamed chunks (ViT-L/14@336)
       const size_t slds = 2 * (size_t)ST_CH * 128 + (size_t)npad * 12;
-      static bool sattr = false;
-      if (!sattr) {
-        CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_stream<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        sattr = true;
-      }
+      CLIPMI_HIP(lds_optin((const void*)attn_bwd_stream<true>, 160 * 1024));
+      CLIPMI_HIP(lds_optin((const void*)attn_bwd_stream<false>, 160 * 1024));
       if (causal) hipLaunchKernelGGL(attn_bwd_stream<true>, dim3(B * H), dim3(512), slds, s, p);
       else hipLaunchKernelGGL(attn_bwd_stream<false>, dim3(B * H), dim3(512), slds, s, p);
     } else if (causal) {
@@ -1444,11 +1420,7 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
   } else {
     AttnF p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D, causal, 0.125f};
     size_t lds = (size_t)F32_CH * 64 * 4 * 2 + (size_t)N * 12;
-    static bool attr = false;
-    if (!attr) {
-      CLIPMI_HIP(hipFuncSetAttribute((const void*)attn_bwd_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
+    CLIPMI_HIP(lds_optin((const void*)attn_bwd_f32, 160 * 1024));
     hipLaunchKernelGGL(attn_bwd_f32, dim3(B * H), dim3(1024), lds, s, p);
   }
   CLIPMI_CHECK_LAUNCH();

@@ -50,6 +50,23 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- MXFP8 (OCP e4m3 + E8M0 per 32-element block), shared by every producer of fp8 operands
+// scale exponent: the smallest e with amax / 2^e <= 448 (e4m3's largest normal), clamped to E8M0
+__device__ __forceinline__ int mx_exponent(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int fe;
+  const float m = frexpf(amax * (1.0f / 448.0f), &fe);  // amax/448 = m * 2^fe, m in [0.5, 1)
+  return max(-127, min(127, m == 0.5f ? fe - 1 : fe));   // ceil(log2(amax / 448))
+}
+// four values * inv -> four e4m3 bytes (round to nearest even, saturated to +-448), little-endian
+__device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d, float inv) {
+  int pk = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a * inv, -448.f), 448.f), fminf(fmaxf(b * inv, -448.f), 448.f),
+                                           0, false);
+  pk = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c * inv, -448.f), 448.f), fminf(fmaxf(d * inv, -448.f), 448.f), pk,
+                                       true);
+  return (uint32_t)pk;
+}
+
 // load/store 4 consecutive elements as float
 __device__ __forceinline__ void load4(const float* p, float v[4]) {
   f32x4 t = *(const f32x4*)p; v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstring>
 #include "internal.h"
+#include <atomic>
 
 extern "C" {
 int clipmi_layernorm_fwd(void*, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int, int,
@@ -30,11 +31,12 @@ int clipmi_colsum(void*, int, const void*, int64_t, int, int, float*, int, void*
 int clipmi_attention_fwd(void*, int, const void*, void*, float*, const int64_t*, int, int, int, int, int);
 int clipmi_attention_bwd(void*, int, const void*, const void*, const float*, const void*, void*, const int64_t*, int,
                          int, int, int, int);
+int clipmi_quant_mxfp8(void*, int, const void*, int64_t, int64_t, int, uint8_t*, uint8_t*);
 }
 
 namespace {
 
-size_t esize(int dt) { return dt == CLIPMI_BF16 ? 2 : 4; }
+size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb,
@@ -55,13 +57,16 @@ int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool 
   return clipmi_gemm(s, &d);
 }
 
+// CUs of the calling thread's current device (cached per device; racing first calls store the same value)
 int cu_count() {
-  static int n = 0;
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
   if (!n) {
-    int dev = 0, c = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-    n = c;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
   }
   return n;
 }
@@ -126,9 +131,37 @@ WsPlan plan(const clipmi_encoder_desc* d) {
   return p;
 }
 
+// MXFP8 forward GEMM: C = epi(q8/s8 W^T), A already quantised (q8 [M, K], s8 [M, K/32])
+// (c_scale != NULL: C is written as MXFP8 too, scales [M, N/32] in c_scale)
+int gemm8q(void* s, int M, int N, int K, const void* q8, const void* s8, const void* Wq, const void* Ws, void* C,
+           int64_t ldc, int flags, const void* bias, const void* res, int64_t ldr, uint8_t* c_scale = nullptr) {
+  clipmi_gemm_desc d;
+  memset(&d, 0, sizeof(d));
+  d.M = M; d.N = N; d.K = K;
+  d.A = q8; d.lda = K; d.a_kmajor = 1;
+  d.B = Wq; d.ldb = K; d.b_kmajor = 1;
+  d.a_scale = (const uint8_t*)s8; d.b_scale = (const uint8_t*)Ws;
+  d.C = C; d.ldc = ldc;
+  d.bias = bias; d.residual = res; d.ldr = ldr;
+  d.alpha = 1.f; d.flags = flags;
+  d.ab_dtype = CLIPMI_FP8; d.c_dtype = c_scale ? CLIPMI_FP8 : CLIPMI_BF16; d.bias_dtype = CLIPMI_BF16;
+  d.c_scale = c_scale;
+  d.split_k = 1;
+  return clipmi_gemm(s, &d);
+}
+// the same with A [M, K] bf16 quantised into the q8/s8 scratch first
+int gemm8(void* s, int M, int N, int K, const void* A, int64_t lda, const void* Wq, const void* Ws, void* C,
+          int64_t ldc, int flags, const void* bias, const void* res, int64_t ldr, void* q8, void* s8) {
+  CLIPMI_TRY(clipmi_quant_mxfp8(s, CLIPMI_BF16, A, lda, M, K, (uint8_t*)q8, (uint8_t*)s8));
+  return gemm8q(s, M, N, K, q8, s8, Wq, Ws, C, ldc, flags, bias, res, ldr);
+}
+
 int validate(const clipmi_encoder_desc* d) {
   CLIPMI_REQUIRE(d && d->layers && d->act, "null descriptor");
-  CLIPMI_REQUIRE(d->dtype == CLIPMI_BF16 || d->dtype == CLIPMI_F32, "dtype");
+  CLIPMI_REQUIRE(d->dtype == CLIPMI_BF16 || d->dtype == CLIPMI_F32 || d->dtype == CLIPMI_FP8, "dtype");
+  CLIPMI_REQUIRE(d->dtype != CLIPMI_FP8 || (d->layers8 && d->q8 && d->s8), "fp8 encoder needs layers8 / q8 / s8");
+  CLIPMI_REQUIRE(d->dtype != CLIPMI_FP8 || (d->D % 256 == 0 && d->F % 128 == 0),
+                 "fp8 encoder: hidden size must be a multiple of 256 and the MLP width of 128");
   CLIPMI_REQUIRE(d->D == d->H * 64, "hidden size must be heads * 64");
   CLIPMI_REQUIRE(d->B >= 0 && d->N >= 1 && d->L >= 1, "shape");
   return CLIPMI_OK;
@@ -143,6 +176,33 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
+  if (dt == CLIPMI_FP8) {  // BASELINE config 5: frozen towers, MXFP8 GEMMs, bf16 everything else
+    const int bf = CLIPMI_BF16;
+    // scratch: [R, D] operand (LayerNorm / attention outputs) then [R, F] (fc1 output), each with its scales
+    uint8_t* qa = (uint8_t*)d->q8;
+    uint8_t* sa = (uint8_t*)d->s8;
+    uint8_t* qb = qa + align256((int64_t)R * D);
+    uint8_t* sb = sa + align256((int64_t)R * D / 32);
+    for (int l = 0; l < d->L; ++l) {
+      const clipmi_layer_w& w = d->layers[l];
+      const clipmi_layer_w8& w8 = d->layers8[l];
+      const clipmi_layer_act& a = d->act[l];
+      void* x_out = (l + 1 < d->L) ? d->act[l + 1].x_in : d->x_out;
+      // producers write the next GEMM's MXFP8 operand directly (no bf16 round trip), except the
+      // attention output, quantised by its own pass
+      CLIPMI_TRY(clipmi_layernorm_fwd_mxfp8(s, bf, a.x_in, D, qa, sa, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps));
+      CLIPMI_TRY(gemm8q(s, R, 3 * D, D, qa, sa, w8.qkv_w, w8.qkv_s, a.qkv, 3 * D, CLIPMI_EPI_BIAS, w.qkv_b, nullptr, 0));
+      CLIPMI_TRY(clipmi_attention_fwd(s, bf, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+      CLIPMI_TRY(gemm8(s, R, D, D, a.o, D, w8.out_w, w8.out_s, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b,
+                       a.x_in, D, qa, sa));
+      CLIPMI_TRY(clipmi_layernorm_fwd_mxfp8(s, bf, a.h, D, qa, sa, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps));
+      CLIPMI_TRY(gemm8q(s, R, F, D, qa, sa, w8.fc1_w, w8.fc1_s, qb, F, CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU, w.fc1_b,
+                        nullptr, 0, sb));
+      CLIPMI_TRY(gemm8q(s, R, D, F, qb, sb, w8.fc2_w, w8.fc2_s, x_out, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.fc2_b,
+                        a.h, D));
+    }
+    return CLIPMI_OK;
+  }
   for (int l = 0; l < d->L; ++l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
@@ -174,6 +234,7 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
 // all-reduces each chunk's (contiguous) gradient slice while the next chunk computes.
 extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo) {
   CLIPMI_TRY(validate(d));
+  CLIPMI_REQUIRE(d->dtype != CLIPMI_FP8, "the fp8 encoder is forward-only (frozen towers)");
   CLIPMI_REQUIRE(0 <= layer_lo && layer_lo <= layer_hi && layer_hi <= d->L, "layer range");
   CLIPMI_REQUIRE(d->grads, "encoder_bwd needs gradient destinations");
   const int dt = d->dtype;

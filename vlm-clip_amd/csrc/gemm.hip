@@ -26,12 +26,14 @@
 #include "common.h"
 #include "internal.h"
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 #include <cstdlib>
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+constexpr int E8_B = CLIPMI_EPI_BIAS, E8_R = CLIPMI_EPI_RESID, E8_Q = CLIPMI_EPI_QGELU;
 
 struct GemmP {
   int M, N, K;
@@ -47,6 +49,8 @@ struct GemmP {
   int var;  // 256-kernel main-loop schedule (0 production)
   int vec8; // bf16 C with N, ldc/ldr/ldaux multiples of 8 and C/res/aux/bias 16-B aligned
   int stagger, first_round;  // s_sleep(127) count for half of the first round's workgroups
+  const uint8_t* a_scale; const uint8_t* b_scale;  // MXFP8: E8M0 per 32-element k-block, [rows][K/32]
+  uint8_t* c_scale;                                 // MXFP8 output: E8M0 per 32 columns, [M][N/32]
 };
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
@@ -959,6 +963,279 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
   finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz, STAGE ? smem + wave * 16384 : nullptr);
 }
 
+// ------------------------------------------------------------------ MXFP8 (config 5)
+// Block-scaled fp8 GEMM for the frozen ViT-L/14@336 towers (BASELINE config 5): both operands
+// OCP e4m3 (k-major, [rows][K] bytes) with one E8M0 scale per 32-element k-block of a row
+// ([rows][K/32] bytes: the OCP MX layout), on v_mfma_scale_f32_16x16x128_f8f6f4 (twice the
+// bf16 MFMA rate; the hardware applies both blocks' scales inside the MFMA).  gemm256_kernel's
+// 256x256 tile and 8-wave 2x4 decomposition with a k-step of 128 bytes, i.e. exactly the bf16
+// kernel's LDS images (128-B rows, same swizzle, same DMA pieces); the scales of the next
+// k-step are loaded to registers beside the DMAs.  Epilogues: finish256 (fp32 accumulators in
+// the 16x16 C/D layout, which does not depend on the input format).
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// fragment of 16 rows x 128 k (fp8).  Operand map of v_mfma_scale_f32_16x16x128_f8f6f4, measured
+// (tools/probes/mfma_f8f6f4_layout.hip, profiles/r02_f8f6f4_layout.txt): lane l holds row l & 15,
+// bytes 0-15 = k 16g .. 16g+15 and bytes 16-31 = k 64 + 16g .. 64 + 16g + 15 (g = l >> 4), and its
+// scale operand is the E8M0 scale of row l & 15, k-block g (k 32g .. 32g+31).
+// MXFP8 output (fc1 -> fc2 in the fp8 towers): alpha, bias, activation, then per 32-column
+// block of a row -- the 8-column pieces of lanes mlane + 16q, q = 0..3 (epilogue256_lds's
+// permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3 bytes (8 B per lane).
+template <int EPI>
+__device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);
+  uint8_t* out = (uint8_t*)p.C;
+  const int nsb = p.N >> 5;
+  float bv[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const int n = min(nb + 32 * jp + coff, p.N - 8);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) {
+        load4((const float*)p.bias + n, bv[jp]);
+        load4((const float*)p.bias + n + 4, bv[jp] + 4);
+      } else {
+        load8((const bf16*)p.bias + n, bv[jp]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mb + i * 16 + mlane;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int n = nb + 32 * jp + coff;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+        v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
+        v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+      }
+      float am = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if (HQ) v[r] = quick_gelu(v[r]);
+        if (HG) v[r] = gelu_erf(v[r]);
+        am = fmaxf(am, fabsf(v[r]));
+      }
+      am = fmaxf(am, __shfl_xor(am, 16, 64));
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const int ex = mx_exponent(am);
+      const float inv = ldexpf(1.0f, -ex);
+      const uint32_t w0 = mx_pack4(v[0], v[1], v[2], v[3], inv), w1 = mx_pack4(v[4], v[5], v[6], v[7], inv);
+      if (m < p.M && n < p.N) {
+        *(u32x2*)(out + (int64_t)m * p.ldc + n) = u32x2{w0, w1};
+        if (q == 0) p.c_scale[(int64_t)m * nsb + ((nb + 32 * jp) >> 5)] = (uint8_t)(ex + 127);
+      }
+    }
+  }
+}
+
+// Async per-lane dword load (vmcnt-counted like the stage DMAs, so the ring's counted waits
+// retire it; the compiler does not track it: consumers read it only through asm volatile after
+// such a wait, see gemm_fp8_kernel).
+__device__ __forceinline__ int ld_dword_async(const SRsrc& r, int voff) {
+  int v;
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r.v) : "memory");
+  return v;
+}
+__device__ __forceinline__ int shr_after_wait(int w, int sh) {
+  int o;
+  asm volatile("v_lshrrev_b32 %0, %1, %2" : "=v"(o) : "v"(sh), "v"(w));
+  return o;
+}
+
+// fragment of 16 rows x 128 k from two consecutive 64-k ring stages (lo = k 0..63, hi = 64..127)
+__device__ __forceinline__ i32x8 read_frag8pp(const char* lo, const char* hi, int rb, int lane) {
+  const int off = kimg32_off(rb + (lane & 15), lane >> 4);
+  const i32x4 a = *LDS_PTR(const i32x4, lo + off);
+  const i32x4 b = *LDS_PTR(const i32x4, hi + off);
+  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// gemm_pp_kernel's ring and ping-pong with fp8 operands.  A ring stage holds 64 k (the bf16
+// kernel's 32 KiB [256][64 B] images, DMA'd by the same stage_pp); one k-step of the 16x16x128
+// MFMA consumes two stages (2t, 2t + 1), in four phases of 8 MFMAs (2 of the wave's 8 m-fragments
+// each: 256 cycles, the bf16 kernel's section length, with few enough live fragments that the
+// 128 accumulators fit the 256 registers of two waves per SIMD).  Step t's phase 0 DMAs stage
+// 2t + 3 and phase 1 stage 2t + 4, into the slots of step t - 1's stages (every load section
+// ends with lgkmcnt(0), so those reads retired before the barrier that precedes the first
+// overwrite).  Both groups wait in their phase-3 load section (vmcnt(4): only stage 2t + 4 may
+// still be in flight), so the MFMA sections are straight-line code with no waits or branches
+// (the compiler keeps them in place between the barriers).  E8M0 scales: per step each lane needs
+// one byte per fragment (row lane & 15, k-block 4t + (lane >> 4)); the dword holding the step's
+// 4 blocks of the row is loaded one step ahead, before the step's stage DMA so the same waits
+// retire it, and shifted into place by asm (ordered after the wait) at the step's start.
+template <typename OutT, int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm_fp8_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int T = p.K / 128, ns = 2 * T, kb = p.K / 32, Kh = p.K / 2;
+  // fp8 rows seen as bf16 pairs: stage_pp moves [256 rows][64 B] pieces = 64 fp8 k per stage
+  const bf16* A = (const bf16*)p.A;
+  const bf16* B = (const bf16*)p.B;
+  const int64_t lda = p.lda / 2, ldb = p.ldb / 2;
+  const SRsrc rsa = make_srsrc(p.a_scale, (uint32_t)((int64_t)p.M * kb));  // rows past M read 0
+  const SRsrc rsb = make_srsrc(p.b_scale, (uint32_t)((int64_t)p.N * kb));
+  // this lane's scale rows: A fragment i = row offa + 16 i, B fragment j = row offb + 16 j
+  const int offa = (m0 + wm * 128 + (lane & 15)) * kb, offb = (n0 + wn * 64 + (lane & 15)) * kb;
+  const int sh = 8 * (lane >> 4);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto slot = [&](int st) { return smem + (st % PP_S) * PP_STAGE; };
+  auto issue = [&](int st) {
+    stage_pp<true>(slot(st), A, lda, m0, p.M, st * 32, Kh, wave, lane);
+    stage_pp<true>(slot(st) + 16384, B, ldb, n0, p.N, st * 32, Kh, wave, lane);
+  };
+  int nx[12], sc[12];  // scale words: [0, 8) A fragments, [8, 12) B fragments
+  auto load_scales = [&](int step) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nx[i] = ld_dword_async(rsa, offa + 16 * i * kb + 4 * step);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nx[8 + j] = ld_dword_async(rsb, offb + 16 * j * kb + 4 * step);
+  };
+  load_scales(0);
+#pragma unroll
+  for (int st = 0; st < 3; ++st)
+    if (st < ns) issue(st);
+  pp_vmcnt(ns > 2 ? 4 : 0);  // stages 0, 1 and step 0's scales landed
+  pp_barrier();
+  if (wm == 1) pp_barrier();
+
+  for (int it = 0; it < T; ++it) {
+    const char* lo = slot(2 * it);
+    const char* hi = slot(2 * it + 1);
+    const bool last = 2 * it + 4 >= ns;
+    i32x8 fb[4];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {  // phase = 2 of the wave's 8 m-fragments x all 4 n-fragments
+      // ---- load section
+      i32x8 fa[2];
+      if (ph == 0) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) sc[i] = shr_after_wait(nx[i], sh);  // landed: last step's wait
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = read_frag8pp(lo + 16384, hi + 16384, wn * 64 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = read_frag8pp(lo, hi, wm * 128 + (ph * 2 + i) * 16, lane);
+      if (ph == 0) {
+        if (it + 1 < T) load_scales(it + 1);
+        if (2 * it + 3 < ns) issue(2 * it + 3);
+      }
+      if (ph == 1 && !last) issue(2 * it + 4);
+      if (ph == 3) pp_vmcnt(last ? 0 : 4);  // stage 2t + 3 and step t + 1's scales landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      // ---- MFMA section
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ph * 2 + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              fb[j], fa[i], acc[ph * 2 + i][j], 0, 0, 0, sc[8 + j], 0, sc[ph * 2 + i]);
+      // pin the section's MFMAs before its closing barrier (otherwise they are sunk towards the
+      // loop latch, past barriers, piling several sections' fragments into registers)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[ph * 2 + i][j]));
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (wm == 0) pp_barrier();  // pairs with group 1's leading barrier
+  if constexpr (std::is_same<OutT, uint8_t>::value) epilogue_q8<EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  else finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, 0, smem + wave * 16384);
+}
+
+template <typename OutT, int EPI>
+void launch_fp8(const GemmP& p, hipStream_t s) {
+  (void)lds_optin((const void*)gemm_fp8_kernel<OutT, EPI>, PP_S * PP_STAGE);
+  GemmP q = p;
+  q.tiles_n = (p.N + BT - 1) / BT;
+  q.ntiles = q.tiles_n * ((p.M + BT - 1) / BT);
+  hipLaunchKernelGGL((gemm_fp8_kernel<OutT, EPI>), dim3(q.ntiles), dim3(NT2), PP_S * PP_STAGE, s, q);
+}
+
+const char* dispatch_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, int flags) {
+  if (q8o) {
+    switch (flags) {
+      case E8_B | E8_Q: launch_fp8<uint8_t, E8_B | E8_Q>(p, s); return "gemm_fp8_fwd_bias_qgelu_q8";
+      default: return nullptr;
+    }
+  }
+  if (f32o) {
+    launch_fp8<float, -1>(p, s);
+    return "gemm_fp8";
+  }
+  switch (flags) {
+    case E8_B: launch_fp8<bf16, E8_B>(p, s); return "gemm_fp8_fwd_bias";
+    case E8_B | E8_R: launch_fp8<bf16, E8_B | E8_R>(p, s); return "gemm_fp8_fwd_bias_resid";
+    case E8_B | E8_Q: launch_fp8<bf16, E8_B | E8_Q>(p, s); return "gemm_fp8_fwd_bias_qgelu";
+    case 0: launch_fp8<bf16, 0>(p, s); return "gemm_fp8";
+    default: launch_fp8<bf16, -1>(p, s); return "gemm_fp8_generic";
+  }
+}
+
+// ---- MXFP8 quantisation: one thread per 32-element block of a row.  scale exponent e = the
+// smallest with amax / 2^e <= 448 (e4m3's largest normal), E8M0 byte e + 127; values /2^e
+// rounded to nearest even (v_cvt_pk_fp8_f32, OCP e4m3 on gfx950).
+template <typename T>
+__global__ __launch_bounds__(256) void quant_mxfp8_kernel(const T* x, int64_t ldx, int64_t R, int K, uint8_t* q,
+                                                         uint8_t* sc) {
+  const int nb = K >> 5;
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= R * nb) return;
+  const int64_t r = id / nb;
+  const int blk = (int)(id - r * nb);
+  const T* src = x + r * ldx + blk * 32;
+  float v[32];
+  if constexpr (std::is_same<T, bf16>::value) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 w = *(const bf16x8*)(src + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[8 * c + e] = (float)w[e];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const f32x4 w = *(const f32x4*)(src + 4 * c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * c + e] = w[e];
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  const int ex = mx_exponent(amax);
+  const float inv = ldexpf(1.0f, -ex);
+  uint32_t w[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) w[e] = mx_pack4(v[4 * e], v[4 * e + 1], v[4 * e + 2], v[4 * e + 3], inv);
+  uint8_t* dst = q + r * (int64_t)K + blk * 32;
+  *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+  *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+  sc[r * nb + blk] = (uint8_t)(ex + 127);
+}
+
 // ------------------------------------------------------------------ persistent ping-pong
 // gemm_pp_kernel's schedule over a flattened stream of (tile, k-stage) pairs.  A workgroup
 // walks its tiles gridDim.x apart and the LDS ring runs straight across tile boundaries, so
@@ -1326,23 +1603,13 @@ void launch_bf16(const GemmP& p, int splits, hipStream_t s) {
 
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG, int VAR>
 void launch256v(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  static bool attr = false;  // 128 KiB of dynamic LDS needs the opt-in once per instance
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    attr = true;
-  }
+  (void)lds_optin((const void*)gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>, 131072);
   hipLaunchKernelGGL((gemm256_kernel<AK, BKM, OutT, EPI, BG, VAR>), dim3(p.ntiles * splits), dim3(NT2), 131072, s,
                      p, bias_grad);
 }
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG, int PPV>
 void launch_ppv(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  static bool attr = false;  // the 5-stage ring takes all 160 KiB of LDS
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_S * PP_STAGE);
-    attr = true;
-  }
+  (void)lds_optin((const void*)gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>, PP_S * PP_STAGE);
   hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, OutT, EPI, BG, PPV>), dim3(p.ntiles * splits), dim3(NT2),
                      PP_S * PP_STAGE, s, p, bias_grad);
 }
@@ -1360,23 +1627,13 @@ int num_cus() {
 }
 template <bool AK, bool BKM, typename OutT, int EPI>
 void launch_pps(const GemmP& p, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pps_kernel<AK, BKM, OutT, EPI>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_S * PP_STAGE);
-    attr = true;
-  }
+  (void)lds_optin((const void*)gemm_pps_kernel<AK, BKM, OutT, EPI>, PP_S * PP_STAGE);
   const int grid = std::min(p.ntiles, num_cus());  // one 160 KiB workgroup per CU
   hipLaunchKernelGGL((gemm_pps_kernel<AK, BKM, OutT, EPI>), dim3(grid), dim3(NT2), PP_S * PP_STAGE, s, p);
 }
 template <bool BKM, typename OutT, int EPI>
 void launch_hp(const GemmP& p, hipStream_t s) {
-  static bool attr = false;  // two 64 KiB K-tile buffers
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_hp_kernel<BKM, OutT, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              131072);
-    attr = true;
-  }
+  (void)lds_optin((const void*)gemm_hp_kernel<BKM, OutT, EPI>, 131072);
   hipLaunchKernelGGL((gemm_hp_kernel<BKM, OutT, EPI>), dim3(p.ntiles), dim3(NT2), 131072, s, p);
 }
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
@@ -1502,6 +1759,41 @@ const char* dispatch_bf16(const GemmP& p, int splits, hipStream_t s, bool f32o, 
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
+  if (d->ab_dtype == CLIPMI_FP8) {  // MXFP8 operands (see include/clipmi.h)
+    CLIPMI_REQUIRE(d->a_kmajor && d->b_kmajor, "fp8: both operands k-major");
+    CLIPMI_REQUIRE(d->K % 128 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0, "fp8: K % 128 == 0, lda/ldb % 16 == 0");
+    CLIPMI_REQUIRE(d->a_scale && d->b_scale, "fp8: block scales required");
+    CLIPMI_REQUIRE(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0, "fp8: A/B 16-byte aligned");
+    CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32 || d->c_dtype == CLIPMI_BF16 || d->c_dtype == CLIPMI_FP8, "c_dtype");
+    CLIPMI_REQUIRE(d->split_k <= 1 && !d->bias_grad, "fp8: forward GEMMs only");
+    const bool q8o = d->c_dtype == CLIPMI_FP8;
+    CLIPMI_REQUIRE(!q8o || (d->c_scale && d->ldc == d->N && d->N % 32 == 0 && ((uintptr_t)d->C & 7) == 0),
+                   "fp8 output: c_scale, ldc == N, N % 32 == 0, C 8-byte aligned");
+    if (d->M == 0 || d->N == 0) return CLIPMI_OK;
+    GemmP p;
+    memset(&p, 0, sizeof(p));
+    p.M = d->M; p.N = d->N; p.K = d->K;
+    p.A = d->A; p.lda = d->lda; p.B = d->B; p.ldb = d->ldb;
+    p.C = d->C; p.ldc = d->ldc; p.bias = d->bias; p.res = d->residual; p.ldr = d->ldr;
+    p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
+    p.bias_f32 = d->bias_dtype == CLIPMI_F32;
+    p.k_per_split = d->K;
+    p.a_scale = (const uint8_t*)d->a_scale;
+    p.b_scale = (const uint8_t*)d->b_scale;
+    p.c_scale = d->c_scale;
+    p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
+            ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
+    p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&
+             ((uintptr_t)d->C % 16 == 0) && ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0) &&
+             ((uintptr_t)d->bias % 16 == 0);
+    const double flops = 2.0 * d->M * d->N * d->K;
+    ProfScope ps(s, nullptr, 0.0);
+    const char* label = dispatch_fp8(p, s, d->c_dtype == CLIPMI_F32, q8o, d->flags);
+    if (!label) return clipmi_invalid("fp8 output: supported epilogue flags are bias + quick_gelu");
+    ps.finish(label, flops);
+    CLIPMI_CHECK_LAUNCH();
+    return CLIPMI_OK;
+  }
   const bool bf = d->ab_dtype == CLIPMI_BF16;
   CLIPMI_REQUIRE(bf || d->ab_dtype == CLIPMI_F32, "ab_dtype");
   if (d->M == 0 || d->N == 0) return CLIPMI_OK;
@@ -1616,5 +1908,23 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     }
     CLIPMI_CHECK_LAUNCH();
   }
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_quant_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, int64_t R, int K, uint8_t* q,
+                                  uint8_t* scales) {
+  CLIPMI_REQUIRE(R >= 0 && K % 32 == 0 && K > 0, "quant_mxfp8: K % 32 == 0");
+  CLIPMI_REQUIRE(dtype == CLIPMI_BF16 || dtype == CLIPMI_F32, "quant_mxfp8: bf16 or f32 input");
+  CLIPMI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 15) == 0 && (ldx % 8) == 0, "quant_mxfp8: alignment");
+  const int64_t n = R * (K / 32);
+  if (n == 0) return CLIPMI_OK;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  if (dtype == CLIPMI_BF16)
+    hipLaunchKernelGGL(quant_mxfp8_kernel<bf16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, ldx, R,
+                       K, q, scales);
+  else
+    hipLaunchKernelGGL(quant_mxfp8_kernel<float>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       R, K, q, scales);
+  CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }

@@ -48,10 +48,15 @@ __device__ __forceinline__ void vstore(T* p, const float* o) {
 // twice the bytes are in flight per wave (one row per wave ran at 4.2 TB/s, latency bound).
 constexpr int LN_RPW = 2;
 
-template <typename T, int PS, int NP>
+// Q8: y is written as MXFP8 instead (q8 [R, D] e4m3 bytes, s8 [R, D/32] E8M0): a 32-element
+// block is 8 consecutive lanes' 4-element pieces (PS == 4), max-reduced across those lanes; the
+// fp8 operand of the next GEMM without a bf16 round trip through HBM.
+template <typename T, int PS, int NP, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
                                                      float* mean_out, float* rstd_out, int R, int D, float eps,
-                                                     const T* pos, const T* cls, int period) {
+                                                     const T* pos, const T* cls, int period, uint8_t* q8 = nullptr,
+                                                     uint8_t* s8 = nullptr) {
+  static_assert(!Q8 || PS == 4, "MXFP8 output needs 4-element pieces");
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_RPW;
   if (row0 >= R) return;
@@ -104,11 +109,23 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, in
     vload<T, PS>(b + c, bv);
 #pragma unroll
     for (int rr = 0; rr < LN_RPW; ++rr) {
-      if (row0 + rr >= R) continue;
+      if (row0 + rr >= R) continue;  // wave-uniform
       float o[PS];
 #pragma unroll
       for (int j = 0; j < PS; ++j) o[j] = (v[rr][k][j] - mean[rr]) * rstd[rr] * wv[j] + bv[j];
-      vstore<T, PS>(y + (int64_t)(row0 + rr) * ldy + c, o);
+      if constexpr (Q8) {
+        // lanes 8u .. 8u + 7 hold one 32-element block; the xor-shuffles stay inside it
+        float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        am = fmaxf(am, __shfl_xor(am, 2, 64));
+        am = fmaxf(am, __shfl_xor(am, 4, 64));
+        const int ex = mx_exponent(am);
+        const float inv = ldexpf(1.0f, -ex);
+        *(uint32_t*)(q8 + (int64_t)(row0 + rr) * D + c) = mx_pack4(o[0], o[1], o[2], o[3], inv);
+        if ((lane & 7) == 0) s8[(int64_t)(row0 + rr) * (D >> 5) + (c >> 5)] = (uint8_t)(ex + 127);
+      } else {
+        vstore<T, PS>(y + (int64_t)(row0 + rr) * ldy + c, o);
+      }
     }
   }
   if (lane == 0) {
@@ -463,6 +480,15 @@ void ln_fwd_launch(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, co
                      (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const T*)pos, (const T*)cls, period);
 }
 template <typename T, int PS, int NP>
+void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t* s8, const void* w, const void* b,
+                      float* mean, float* rstd, int R, int D, float eps) {
+  if constexpr (PS == 4) {
+    hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP, true>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s,
+                       (T*)x, ldx, (T*)nullptr, (int64_t)0, (const T*)w, (const T*)b, mean, rstd, R, D, eps,
+                       (const T*)nullptr, (const T*)nullptr, 1, q8, s8);
+  }
+}
+template <typename T, int PS, int NP>
 void ln_bwd_launch(hipStream_t s, int grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                    int64_t ldres, float* ws, int R, int D) {
@@ -497,6 +523,19 @@ extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ld
   if (R == 0) return CLIPMI_OK;
   if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_fwd_launch, bf16, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
   else LN_DISPATCH(D, ln_fwd_launch, float, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, uint8_t* q8,
+                                          uint8_t* s8, const void* w, const void* b, float* mean, float* rstd, int R,
+                                          int D, float eps) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(dtype == CLIPMI_BF16, "layernorm_fwd_mxfp8: bf16 input");
+  CLIPMI_REQUIRE(D % 256 == 0 && D <= 1024, "layernorm_fwd_mxfp8: D must be a multiple of 256, <= 1024");
+  CLIPMI_REQUIRE(q8 && s8, "layernorm_fwd_mxfp8: outputs");
+  if (R == 0) return CLIPMI_OK;
+  LN_DISPATCH(D, ln_fwd_q8_launch, bf16, s, (void*)x, ldx, q8, s8, w, b, mean, rstd, R, D, eps);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
