@@ -12,7 +12,8 @@ from clipmi import kernels as K, _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 R, D, F = B * 577, 1024, 4096
-REPS = 10
+REPS = int(os.environ.get("FP8_REPS", "10"))
+ONLY = os.environ.get("FP8_SHAPES", "").split(",") if os.environ.get("FP8_SHAPES") else None
 
 
 def timeit(f, n=REPS):
@@ -34,12 +35,27 @@ def mx(r, c):
 
 
 torch.manual_seed(0)
+if os.environ.get("FP8_KSWEEP"):  # time(K) = per-tile fixed cost + K/64 stages: split them (N = 3072, bias)
+    for Kd in (128, 256, 512, 1024, 2048, 4096):
+        x = (torch.randn(R, Kd, device="cuda") * 0.5).to(torch.bfloat16)
+        w = (torch.randn(3 * D, Kd, device="cuda") * 0.02).to(torch.bfloat16)
+        bias = torch.randn(3 * D, device="cuda").to(torch.bfloat16)
+        A, Bq = K.quant_mxfp8(x), K.quant_mxfp8(w)
+        C = torch.empty(R, 3 * D, device="cuda", dtype=torch.bfloat16)
+        ms8 = timeit(lambda: K.gemm_fp8(R, 3 * D, Kd, A, Bq, C, 3 * D, bias=bias, flags=_lib.EPI_BIAS))
+        msb = timeit(lambda: K.gemm(R, 3 * D, Kd, x, Kd, True, w, Kd, True, C, 3 * D, bias=bias, flags=_lib.EPI_BIAS))
+        print(f"ksweep K={Kd:5d}: fp8 {ms8 * 1e3:8.1f} us  bf16 {msb * 1e3:8.1f} us", flush=True)
+        del x, w, A, Bq, C
+        torch.cuda.empty_cache()
+    sys.exit(0)
 QGB = _lib.EPI_BIAS | _lib.EPI_QGELU
 for name, N, Kd, flags, q8o in (("qkv", 3 * D, D, _lib.EPI_BIAS, False),
                                 ("out", D, D, _lib.EPI_BIAS | _lib.EPI_RESID, False),
                                 ("fc1", F, D, QGB, False),
                                 ("fc1_q8", F, D, QGB, True),
                                 ("fc2", D, F, _lib.EPI_BIAS | _lib.EPI_RESID, False)):
+    if ONLY and name not in ONLY:
+        continue
     x = (torch.randn(R, Kd, device="cuda") * 0.5).to(torch.bfloat16)
     w = (torch.randn(N, Kd, device="cuda") * 0.02).to(torch.bfloat16)
     bias = torch.randn(N, device="cuda").to(torch.bfloat16)
@@ -59,6 +75,8 @@ for name, N, Kd, flags, q8o in (("qkv", 3 * D, D, _lib.EPI_BIAS, False),
     del x, w, A, Bq, C, res
     torch.cuda.empty_cache()
 
+if ONLY:
+    sys.exit(0)
 x = torch.randn(R, D, device="cuda").to(torch.bfloat16)
 wl = torch.ones(D, device="cuda", dtype=torch.bfloat16)
 bl = torch.zeros(D, device="cuda", dtype=torch.bfloat16)

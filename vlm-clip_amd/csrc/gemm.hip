@@ -832,6 +832,8 @@ __device__ __forceinline__ void pp_barrier() {
 // wait until at most n of this wave's DMAs are outstanding (n even, 0..8)
 __device__ __forceinline__ void pp_vmcnt(int n) {
   switch (n) {
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
@@ -966,18 +968,43 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
 // ------------------------------------------------------------------ MXFP8 (config 5)
 // Block-scaled fp8 GEMM for the frozen ViT-L/14@336 towers (BASELINE config 5): both operands
 // OCP e4m3 (k-major, [rows][K] bytes) with one E8M0 scale per 32-element k-block of a row
-// ([rows][K/32] bytes: the OCP MX layout), on v_mfma_scale_f32_16x16x128_f8f6f4 (twice the
-// bf16 MFMA rate; the hardware applies both blocks' scales inside the MFMA).  gemm256_kernel's
-// 256x256 tile and 8-wave 2x4 decomposition with a k-step of 128 bytes, i.e. exactly the bf16
-// kernel's LDS images (128-B rows, same swizzle, same DMA pieces); the scales of the next
-// k-step are loaded to registers beside the DMAs.  Epilogues: finish256 (fp32 accumulators in
-// the 16x16 C/D layout, which does not depend on the input format).
+// ([rows][K/32] bytes: the OCP MX layout), on v_mfma_scale_f32_32x32x64_f8f6f4 (twice the bf16
+// MFMA rate; the hardware applies both operands' block scales inside the MFMA).  Epilogues: the
+// bf16 kernels' finish256 after a register-layout conversion, or MXFP8 output (epilogue_q8).
 typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-// fragment of 16 rows x 128 k (fp8).  Operand map of v_mfma_scale_f32_16x16x128_f8f6f4, measured
-// (tools/probes/mfma_f8f6f4_layout.hip, profiles/r02_f8f6f4_layout.txt): lane l holds row l & 15,
-// bytes 0-15 = k 16g .. 16g+15 and bytes 16-31 = k 64 + 16g .. 64 + 16g + 15 (g = l >> 4), and its
-// scale operand is the E8M0 scale of row l & 15, k-block g (k 32g .. 32g+31).
+// Operand map of v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3), measured with exact data
+// (tools/probes/mfma_f8f6f4_32x32_layout.hip, profiles/r02_f8f6f4_32x32_layout.txt): lane l holds
+// row l & 31; its bytes 0-15 belong to k-block 0 and bytes 16-31 to k-block 1 (32 k each), the two
+// lane halves h = l >> 5 splitting each block, and its scale operand is the E8M0 scale of row l & 31,
+// block h.  So with k 16h .. 16h+15 in bytes 0-15 and k 32 + 16h .. in bytes 16-31 (the same map for
+// both operands), one 64-k ring stage is exactly one MFMA k-step.  (16x16x128 would consume two
+// stages per MFMA, halving the ring's prefetch depth: measured at the bf16 kernel's rate only.)
+// fp8 stage images use the swizzle chunk ^ ((row >> 2) & 3), conflict-free for this 32-row read.
+__device__ __forceinline__ int kimg8_off(int r, int c) { return r * 64 + ((c ^ (r >> 2)) & 3) * 16; }
+
+__device__ __forceinline__ i32x8 read_frag8(const char* img, int rb, int lane) {
+  const int r = rb + (lane & 31), h = lane >> 5;
+  const i32x4 a = *LDS_PTR(const i32x4, img + kimg8_off(r, h));
+  const i32x4 b = *LDS_PTR(const i32x4, img + kimg8_off(r, 2 + h));
+  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// stage_pp<true> for fp8 rows (64 B = 64 k per row and stage) with the fp8 swizzle
+__device__ __forceinline__ void stage_pp8(char* img, const uint8_t* X, int64_t ld, int row0, int R, int k0, int wave,
+                                          int lane) {
+  const int rows = min(BT, R - row0);
+  const SRsrc rs = make_srsrc(X + (int64_t)row0 * ld + k0, rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld + 64) : 0u);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = wave * 2 + i;  // 0..15, 1 KiB = 16 rows each
+    const int r = 16 * j + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    dma16(rs, img + j * 1024, (int)((int64_t)r * ld + c * 16));
+  }
+}
+
 // MXFP8 output (fc1 -> fc2 in the fp8 towers): alpha, bias, activation, then per 32-column
 // block of a row -- the 8-column pieces of lanes mlane + 16q, q = 0..3 (epilogue256_lds's
 // permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3 bytes (8 B per lane).
@@ -1051,27 +1078,18 @@ __device__ __forceinline__ int shr_after_wait(int w, int sh) {
   return o;
 }
 
-// fragment of 16 rows x 128 k from two consecutive 64-k ring stages (lo = k 0..63, hi = 64..127)
-__device__ __forceinline__ i32x8 read_frag8pp(const char* lo, const char* hi, int rb, int lane) {
-  const int off = kimg32_off(rb + (lane & 15), lane >> 4);
-  const i32x4 a = *LDS_PTR(const i32x4, lo + off);
-  const i32x4 b = *LDS_PTR(const i32x4, hi + off);
-  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
-
-// gemm_pp_kernel's ring and ping-pong with fp8 operands.  A ring stage holds 64 k (the bf16
-// kernel's 32 KiB [256][64 B] images, DMA'd by the same stage_pp); one k-step of the 16x16x128
-// MFMA consumes two stages (2t, 2t + 1), in four phases of 8 MFMAs (2 of the wave's 8 m-fragments
-// each: 256 cycles, the bf16 kernel's section length, with few enough live fragments that the
-// 128 accumulators fit the 256 registers of two waves per SIMD).  Step t's phase 0 DMAs stage
-// 2t + 3 and phase 1 stage 2t + 4, into the slots of step t - 1's stages (every load section
-// ends with lgkmcnt(0), so those reads retired before the barrier that precedes the first
-// overwrite).  Both groups wait in their phase-3 load section (vmcnt(4): only stage 2t + 4 may
-// still be in flight), so the MFMA sections are straight-line code with no waits or branches
-// (the compiler keeps them in place between the barriers).  E8M0 scales: per step each lane needs
-// one byte per fragment (row lane & 15, k-block 4t + (lane >> 4)); the dword holding the step's
-// 4 blocks of the row is loaded one step ahead, before the step's stage DMA so the same waits
-// retire it, and shifted into place by asm (ordered after the wait) at the step's start.
+// gemm_pp_kernel's schedule with fp8 operands on v_mfma_scale_f32_32x32x64_f8f6f4: the same
+// 256x256 tile, 8 waves (2 along M x 4 along N, 128x64 each = 4 x 2 blocks of 32x32), the same
+// 5-slot ring of 32 KiB stages (here 64 k each) with 3 stages of prefetch, the same two
+// ping-pong phases per stage (m-half: 2 A blocks x 2 B blocks = 4 MFMAs of 64 cycles, the bf16
+// section length) and the same counted waits, so the prefetch depth in time equals the bf16
+// kernel's while each stage carries twice the k.  E8M0 scales: a lane needs, per stage
+// s = 2t + u, byte 2s + h of its row's scales; the dword of blocks 4t .. 4t+3 serves both stages
+// of pair t.  It is loaded two pairs ahead (at stage 2t - 4, before that stage's DMA; loaded one
+// pair ahead its latency was exposed every pair: 0.6 of the bf16 kernel's stage rate), retired by
+// the stage waits, and shifted into both stages' scale registers by asm at the pair's start.
+// The MFMA sections are pinned before their closing barrier (asm "+v" on the accumulators),
+// else they are sunk towards the loop latch past barriers.
 template <typename OutT, int EPI>
 __global__ __launch_bounds__(NT2, 1) void gemm_fp8_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1081,65 +1099,88 @@ __global__ __launch_bounds__(NT2, 1) void gemm_fp8_kernel(GemmP p) {
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BT, n0 = tn * BT;
-  const int T = p.K / 128, ns = 2 * T, kb = p.K / 32, Kh = p.K / 2;
-  // fp8 rows seen as bf16 pairs: stage_pp moves [256 rows][64 B] pieces = 64 fp8 k per stage
-  const bf16* A = (const bf16*)p.A;
-  const bf16* B = (const bf16*)p.B;
-  const int64_t lda = p.lda / 2, ldb = p.ldb / 2;
+  const int ns = p.K / 64, T = p.K / 128, kb = p.K / 32;
+  const uint8_t* A = (const uint8_t*)p.A;
+  const uint8_t* B = (const uint8_t*)p.B;
   const SRsrc rsa = make_srsrc(p.a_scale, (uint32_t)((int64_t)p.M * kb));  // rows past M read 0
   const SRsrc rsb = make_srsrc(p.b_scale, (uint32_t)((int64_t)p.N * kb));
-  // this lane's scale rows: A fragment i = row offa + 16 i, B fragment j = row offb + 16 j
-  const int offa = (m0 + wm * 128 + (lane & 15)) * kb, offb = (n0 + wn * 64 + (lane & 15)) * kb;
-  const int sh = 8 * (lane >> 4);
+  const int offa = (m0 + wm * 128 + (lane & 31)) * kb, offb = (n0 + wn * 64 + (lane & 31)) * kb;
+  const int h = lane >> 5;
 
-  f32x4 acc[8][4];
+  f32x16 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   auto slot = [&](int st) { return smem + (st % PP_S) * PP_STAGE; };
-  auto issue = [&](int st) {
-    stage_pp<true>(slot(st), A, lda, m0, p.M, st * 32, Kh, wave, lane);
-    stage_pp<true>(slot(st) + 16384, B, ldb, n0, p.N, st * 32, Kh, wave, lane);
-  };
-  int nx[12], sc[12];  // scale words: [0, 8) A fragments, [8, 12) B fragments
-  auto load_scales = [&](int step) {
+  // scale words of pair t (stages 2t, 2t + 1) in nx[t & 1]: [0, 4) A blocks, [4, 6) B blocks;
+  // sc[u] = stage 2t + u's bytes.  Pair t + 2's words are loaded at stage 2t, so the stage DMA
+  // waits retire them two stages before use, like the stages themselves.
+  int nx[2][6], sc[2][6];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) nx[i] = ld_dword_async(rsa, offa + 16 * i * kb + 4 * step);
+  for (int a = 0; a < 4; ++a) nx[0][a] = ld_dword_async(rsa, offa + 32 * a * kb);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) nx[8 + j] = ld_dword_async(rsb, offb + 16 * j * kb + 4 * step);
-  };
-  load_scales(0);
+  for (int b = 0; b < 2; ++b) nx[0][4 + b] = ld_dword_async(rsb, offb + 32 * b * kb);
+  if (T > 1) {
 #pragma unroll
-  for (int st = 0; st < 3; ++st)
-    if (st < ns) issue(st);
-  pp_vmcnt(ns > 2 ? 4 : 0);  // stages 0, 1 and step 0's scales landed
+    for (int a = 0; a < 4; ++a) nx[1][a] = ld_dword_async(rsa, offa + 32 * a * kb + 4);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) nx[1][4 + b] = ld_dword_async(rsb, offb + 32 * b * kb + 4);
+  }
+#pragma unroll
+  for (int st = 0; st < PP_D; ++st) {
+    if (st < ns) {
+      stage_pp8(slot(st), A, p.lda, m0, p.M, st * 64, wave, lane);
+      stage_pp8(slot(st) + 16384, B, p.ldb, n0, p.N, st * 64, wave, lane);
+    }
+  }
+  pp_vmcnt(4 * (min(PP_D, ns) - 1));  // stage 0 and pairs 0, 1's scales landed
   pp_barrier();
   if (wm == 1) pp_barrier();
 
-  for (int it = 0; it < T; ++it) {
-    const char* lo = slot(2 * it);
-    const char* hi = slot(2 * it + 1);
-    const bool last = 2 * it + 4 >= ns;
-    i32x8 fb[4];
+  // one stage; UU = st % 4 is a template constant so the scale-buffer parity (pair t % 2 = UU / 2)
+  // and the stage parity index register arrays statically (a runtime index would demote them to
+  // scratch, which an asm-written async register must never be)
+  auto stage = [&](auto UU, int st) {
+    constexpr int uu = decltype(UU)::value, u = uu & 1, pb = uu >> 1;
+    const char* img = slot(st);
+    const bool issue = st + PP_D < ns;
+    const int kn = (st + PP_D) * 64;
+    i32x8 fb[2];
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {  // phase = 2 of the wave's 8 m-fragments x all 4 n-fragments
+    for (int ph = 0; ph < 2; ++ph) {
       // ---- load section
+      if (ph == 0) {
+        if constexpr (u == 0) {  // pair start: both stages' scale bytes, then pair t + 2's words
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            sc[0][i] = shr_after_wait(nx[pb][i], 8 * h);
+            sc[1][i] = shr_after_wait(nx[pb][i], 16 + 8 * h);
+          }
+          if (st + 4 < ns) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a) nx[pb][a] = ld_dword_async(rsa, offa + 32 * a * kb + 4 * (st / 2 + 2));
+#pragma unroll
+            for (int b = 0; b < 2; ++b) nx[pb][4 + b] = ld_dword_async(rsb, offb + 32 * b * kb + 4 * (st / 2 + 2));
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) fb[b] = read_frag8(img + 16384, wn * 64 + b * 32, lane);
+      }
       i32x8 fa[2];
-      if (ph == 0) {
 #pragma unroll
-        for (int i = 0; i < 12; ++i) sc[i] = shr_after_wait(nx[i], sh);  // landed: last step's wait
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag8pp(lo + 16384, hi + 16384, wn * 64 + j * 16, lane);
+      for (int i = 0; i < 2; ++i) fa[i] = read_frag8(img, wm * 128 + (ph * 2 + i) * 32, lane);
+      if (issue) {
+        if (ph == 0) stage_pp8(slot(st + PP_D), A, p.lda, m0, p.M, kn, wave, lane);
+        else stage_pp8(slot(st + PP_D) + 16384, B, p.ldb, n0, p.N, kn, wave, lane);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = read_frag8pp(lo, hi, wm * 128 + (ph * 2 + i) * 16, lane);
-      if (ph == 0) {
-        if (it + 1 < T) load_scales(it + 1);
-        if (2 * it + 3 < ns) issue(2 * it + 3);
+      if (ph == 1) {  // stage st + 1 landed; allowed in flight: stages st + 2, st + 3 and the
+                      // scale words loaded at this pair's even stage (issued after st + 1's DMA)
+        const bool wl = u == 0 ? st + 4 < ns : st + 3 < ns;
+        pp_vmcnt(4 * (st + 2 < ns) + 4 * (st + 3 < ns) + (wl ? 6 : 0));
       }
-      if (ph == 1 && !last) issue(2 * it + 4);
-      if (ph == 3) pp_vmcnt(last ? 0 : 4);  // stage 2t + 3 and step t + 1's scales landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
       // ---- MFMA section
@@ -1147,22 +1188,56 @@ __global__ __launch_bounds__(NT2, 1) void gemm_fp8_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[ph * 2 + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              fb[j], fa[i], acc[ph * 2 + i][j], 0, 0, 0, sc[8 + j], 0, sc[ph * 2 + i]);
-      // pin the section's MFMAs before its closing barrier (otherwise they are sunk towards the
-      // loop latch, past barriers, piling several sections' fragments into registers)
+        for (int b = 0; b < 2; ++b)
+          acc[ph * 2 + i][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              fb[b], fa[i], acc[ph * 2 + i][b], 0, 0, 0, sc[u][4 + b], 0, sc[u][ph * 2 + i]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[ph * 2 + i][j]));
+        for (int b = 0; b < 2; ++b) asm volatile("" : "+v"(acc[ph * 2 + i][b]));
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
     }
+  };
+  for (int st0 = 0; st0 < ns; st0 += 4) {  // ns is even: stages st0, st0 + 1 always exist
+    stage(std::integral_constant<int, 0>{}, st0);
+    stage(std::integral_constant<int, 1>{}, st0 + 1);
+    if (st0 + 2 < ns) {
+      stage(std::integral_constant<int, 2>{}, st0 + 2);
+      stage(std::integral_constant<int, 3>{}, st0 + 3);
+    }
   }
   if (wm == 0) pp_barrier();  // pairs with group 1's leading barrier
-  if constexpr (std::is_same<OutT, uint8_t>::value) epilogue_q8<EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
-  else finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, 0, smem + wave * 16384);
+  // 32x32 accumulator blocks -> the 16x16 fragment layout of the shared epilogues, through the
+  // wave's 16 KiB of the (idle) ring, 64 rows at a time: lane l holds m = 32a + (l & 31),
+  // n = 32b + 8q + 4h + (0..3) in registers 4q..4q+3 of block (a, b); [64][64] fp32 rows of 256 B,
+  // 16-B chunk c of row r at c ^ (r & 15).
+  char* st_w = smem + wave * 16384;
+  f32x4 acc16[8][4];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 32 * a2 + (lane & 31), c = 8 * b + 2 * q + h;
+          const f32x16& v = acc[2 * hf + a2][b];
+          *LDS_PTR(f32x4, st_w + r * 256 + ((c ^ (r & 15)) << 4)) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * i2 + (lane & 15), c = 4 * j + (lane >> 4);
+        acc16[4 * hf + i2][j] = *LDS_PTR(const f32x4, st_w + r * 256 + ((c ^ (r & 15)) << 4));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if constexpr (std::is_same<OutT, uint8_t>::value) epilogue_q8<EPI>(p, acc16, m0 + wm * 128, n0 + wn * 64, lane);
+  else finish256<OutT, EPI>(p, acc16, m0 + wm * 128, n0 + wn * 64, lane, 0, st_w);
 }
 
 template <typename OutT, int EPI>
