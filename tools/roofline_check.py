@@ -1,5 +1,5 @@
 """Cross-check bench.py's live roofline timing against a rocprofv3 kernel trace of the same
-command: mean duration of the roofline kernel's launches on the caller's stream (the stream the
+command: mean duration of each GEMM family's launches on the caller's stream (the stream the
 vision attention kernel runs on; the text tower has its own).  Usage: roofline_check.py TRACE.csv"""
 import csv, sys
 from collections import defaultdict
@@ -10,10 +10,13 @@ for r in rows:
     if "attn_fwd_pf<14" in r["Kernel_Name"]:
         main = r["Stream_Id"]
         break
-dur = defaultdict(list)
-for r in rows:
-    if "gemm256_kernel<false, false, float, 0," in r["Kernel_Name"]:
-        dur[r["Stream_Id"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-for sid, d in dur.items():
-    tag = "caller's stream (timed live)" if sid == main else "side stream"
-    print(f"stream {sid} [{tag}]: {len(d)} wgrad launches, mean {sum(d) / len(d):.4f} ms")
+FAMILIES = {"gemm256_wgrad": ("gemm256_kernel<false, false, float, 0,", "gemm256_kernelILb0ELb0EfLi0E"),
+            "gemm256_fwd_dgrad": ("gemm_pp_kernel",)}
+for fam, pats in FAMILIES.items():
+    dur = defaultdict(list)
+    for r in rows:
+        if any(p in r["Kernel_Name"] for p in pats):
+            dur[r["Stream_Id"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    for sid, d in dur.items():
+        tag = "caller's stream (timed live)" if sid == main else "side stream"
+        print(f"{fam} stream {sid} [{tag}]: {len(d)} launches, mean {sum(d) / len(d):.4f} ms")

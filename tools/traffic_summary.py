@@ -1,41 +1,57 @@
-"""Per-launch HBM bytes of the roofline kernel family from rocprofv3 FETCH_SIZE / WRITE_SIZE
-passes (counter_collection.csv, values in KiB), over the launches bench.py's live roofline
-times: the vision tower's (the caller's stream; the text tower runs on a second stream).  The
-passes run with CLIPMI_OVERLAP=0, so each step's 97 wgrad launches come in program order: the
-vision backward's 48 encoder wgrads + the patch embedding, then the text tower's 48.  gfx950 FETCH_SIZE counts 128-B requests as
-64 B (MI355X_MICROARCH.md §HBM): the wgrad kernel's LDS-DMA pieces are whole 128-B lines
-(4 k-rows x 256 B), so fetched bytes = 2 x FETCH_SIZE.  WRITE_SIZE is exact for its 16-B
-per-lane slab stores.  Usage: traffic_summary.py FETCH_DIR WRITE_DIR OUT.json"""
+"""Per-launch HBM bytes of bench.py's GEMM families (wgrad, forward+dgrad) from rocprofv3
+FETCH_SIZE / WRITE_SIZE passes (counter_collection.csv, values in KiB), over the launches
+bench.py's live roofline times: the vision tower's (the caller's stream; the text tower runs on
+a second stream).  gfx950 FETCH_SIZE counts 128-B requests as 64 B (MI355X_MICROARCH.md §HBM),
+so fetched bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B-per-lane stores.
+Usage: traffic_summary.py FETCH_DIR WRITE_DIR OUT_PREFIX"""
 import csv, glob, json, os, sys
 
-KERNEL = "gemm256_kernel<false, false, float, 0,"  # "gemm256_wgrad_splitk" in libclipmi's labels
-LABEL = "gemm256_wgrad_splitk"
+FAMILIES = {
+    # wgrad: split-K gemm256 kernel; with CLIPMI_OVERLAP=0 each step's 97 launches come in program
+    # order, the vision backward's 48 encoder wgrads + the patch embedding first
+    "gemm256_wgrad": "gemm256_kernel<false, false, float, 0,",
+    # forward + dgrad: every gemm_pp_kernel instantiation; the vision tower's launches are the ones
+    # whose grid is a multiple of its M tiles (B=1024: 201,728 rows = 788 tiles of 256)
+    "gemm256_fwd_dgrad": "gemm_pp_kernel",  # demangled or mangled names
+}
+PER_STEP, VISION, M_TILES = 97, 49, 788
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kernel):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    out = {}
+    out, grid = {}, {}
     for r in csv.DictReader(open(f)):
-        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             out[r["Dispatch_Id"]] = out.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return list(out.values())
+            grid[r["Dispatch_Id"]] = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
+    ids = sorted(out, key=int)
+    return [out[i] for i in ids], [grid[i] for i in ids]
 
 
-PER_STEP, VISION = 97, 49
+def vision_only(family, vals, grids):
+    if family == "gemm256_wgrad":
+        assert len(vals) % PER_STEP == 0, f"{len(vals)} wgrad launches is not a whole number of steps"
+        return [v for i, v in enumerate(vals) if i % PER_STEP < VISION]
+    return [v for v, g in zip(vals, grids) if g % M_TILES == 0]
 
 
-def vision_only(vals):
-    assert len(vals) % PER_STEP == 0, f"{len(vals)} wgrad launches is not a whole number of steps"
-    return [v for i, v in enumerate(vals) if i % PER_STEP < VISION]
+def summarize(family, fetch_dir, write_dir):
+    k = FAMILIES[family]
+    fetch = vision_only(family, *per_dispatch(fetch_dir, "FETCH_SIZE", k))
+    write = vision_only(family, *per_dispatch(write_dir, "WRITE_SIZE", k))
+    rd = 2.0 * 1024 * sum(fetch) / len(fetch)
+    wr = 1024.0 * sum(write) / len(write)
+    return {"kernel": family, "launches": [len(fetch), len(write)], "read_bytes_per_launch": rd,
+            "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
+            "subset": "vision tower launches (the ones bench.py's live roofline times on the caller's stream)",
+            "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over CLIPMI_OVERLAP=0 bench.py "
+                      "--steps 2 --warmup 1; FETCH_SIZE x2 (gfx950 tallies 128-B requests as 64 B; the guide's "
+                      "calibration is for 16-B-per-lane streaming reads, which these LDS-DMA pieces are), KiB -> bytes"}
 
 
-fetch = vision_only(per_dispatch(sys.argv[1], "FETCH_SIZE"))
-write = vision_only(per_dispatch(sys.argv[2], "WRITE_SIZE"))
-rd = 2.0 * 1024 * sum(fetch) / len(fetch)
-wr = 1024.0 * sum(write) / len(write)
-res = {"kernel": LABEL, "launches": [len(fetch), len(write)], "read_bytes_per_launch": rd,
-       "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
-       "subset": "vision tower launches (first 49 of each step's 97)",
-       "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over CLIPMI_OVERLAP=0 bench.py "
-                 "--steps 2 --warmup 1; FETCH_SIZE x2 (gfx950 reports 128-B requests as 64 B), KiB -> bytes"}
-json.dump(res, open(sys.argv[3], "w"), indent=1)
+if __name__ == "__main__":
+    # traffic_summary.py FETCH_DIR WRITE_DIR OUT_PREFIX  ->  OUT_PREFIX_wgrad.json, OUT_PREFIX_fwd_dgrad.json
+    for fam, suffix in (("gemm256_wgrad", "wgrad"), ("gemm256_fwd_dgrad", "fwd_dgrad")):
+        res = summarize(fam, sys.argv[1], sys.argv[2])
+        json.dump(res, open(f"{sys.argv[3]}_{suffix}.json", "w"), indent=1)
+        print(fam, json.dumps(res))
