@@ -103,7 +103,9 @@ __device__ __forceinline__ SRsrc make_srsrc(const void* base, uint32_t num_recor
 }
 __device__ __forceinline__ void dma16(SRsrc r, char* lds_wave_base, int voff) {
   const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, lds_wave_base);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r.v)
+  // s_nop 2 + s_mov + s_nop 0: the 5 wait states a buffer instruction needs after a VALU
+  // (v_readfirstlane in make_srsrc) wrote its descriptor SGPRs; hipcc pads nothing inside asm
+  asm volatile("s_nop 2\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r.v)
                : "memory");
 }
 

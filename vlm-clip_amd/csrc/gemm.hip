@@ -51,7 +51,25 @@ struct GemmP {
   int stagger, first_round;  // s_sleep(127) count for half of the first round's workgroups
   const uint8_t* a_scale; const uint8_t* b_scale;  // MXFP8: E8M0 per 32-element k-block, [rows][K/32]
   uint8_t* c_scale;                                 // MXFP8 output: E8M0 per 32 columns, [M][N/32]
+  int raster;  // 0: tiles row-major; g > 0: g tile-rows at a time, column by column (tile_coords)
 };
+
+// tile -> (tm, tn).  Row-major, or grouped: g tile-rows at a time, walked column by column, so
+// the ~32 tiles an XCD holds at once (its contiguous share of the XCD-remapped ids) share g A
+// panels and a few B panels in its 4 MB L2 instead of streaming every B panel per tile-row.
+__device__ __forceinline__ void tile_coords(const GemmP& p, int tile, int& tm, int& tn) {
+  if (p.raster > 0) {
+    const int g = p.raster, tiles_m = p.ntiles / p.tiles_n;
+    const int grp = tile / (g * p.tiles_n);
+    const int rem = tile - grp * g * p.tiles_n;
+    const int rows = min(g, tiles_m - grp * g);
+    tn = rem / rows;
+    tm = grp * g + (rem - tn * rows);
+  } else {
+    tm = tile / p.tiles_n;
+    tn = tile - tm * p.tiles_n;
+  }
+}
 
 __device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
   return p.bias_f32 ? ((const float*)p.bias)[n] : (float)((const bf16*)p.bias)[n];
@@ -856,7 +874,8 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
   // tiles of one k-slab, so that slab's A and B panels are fetched into its L2 once
   const int wid = xcd_remap(blockIdx.x, gridDim.x);
   const int kz = wid / p.ntiles, tile = wid - kz * p.ntiles;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn;
+  tile_coords(p, tile, tm, tn);
   const int m0 = tm * BT, n0 = tn * BT;
   const int kbeg = kz * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
@@ -1069,7 +1088,7 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[8][4], 
 // such a wait, see gemm_fp8_kernel).
 __device__ __forceinline__ int ld_dword_async(const SRsrc& r, int voff) {
   int v;
-  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r.v) : "memory");
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r.v) : "memory");
   return v;
 }
 __device__ __forceinline__ int shr_after_wait(int w, int sh) {
@@ -1097,7 +1116,8 @@ __global__ __launch_bounds__(NT2, 1) void gemm_fp8_kernel(GemmP p) {
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn;
+  tile_coords(p, tile, tm, tn);
   const int m0 = tm * BT, n0 = tn * BT;
   const int ns = p.K / 64, T = p.K / 128, kb = p.K / 32;
   const uint8_t* A = (const uint8_t*)p.A;
@@ -1829,6 +1849,17 @@ const char* dispatch_bf16(const GemmP& p, int splits, hipStream_t s, bool f32o, 
   return "gemm_generic";
 }
 
+// tile-rows per raster group of the 256x256 kernels; CLIPMI_RASTER overrides (0 = row-major).
+// Defaults from profiles/r02_raster_ab.log: bf16 row-major (groups of 4/8/16: within +-3 %, no
+// consistent winner), fp8 groups of 8 (fc1 +10 %, the rest neutral).
+int raster_rows(bool fp8 = false) {
+  static const int r = [] {
+    const char* e = getenv("CLIPMI_RASTER");
+    return e ? atoi(e) : -1;
+  }();
+  return r >= 0 ? r : (fp8 ? 8 : 0);
+}
+
 }  // namespace
 
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
@@ -1856,6 +1887,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     p.a_scale = (const uint8_t*)d->a_scale;
     p.b_scale = (const uint8_t*)d->b_scale;
     p.c_scale = d->c_scale;
+    p.raster = raster_rows(true);
     p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
             ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
     p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&
@@ -1905,6 +1937,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }();
   const bool wlayout = !d->a_kmajor && !d->b_kmajor;
   const int evar = wlayout ? env_wvar : env_var;
+  p.raster = raster_rows();
   p.stagger = 0;
   p.first_round = num_cus();
   if (d->force_small_tile >= 100) {  // A/B hook: 1xx ping-pong, 2xx persistent, with a stagger of xx
