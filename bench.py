@@ -40,6 +40,7 @@ from clipmi import config as C  # noqa: E402
 METRIC = "image-text pairs/sec, ViT-B/16 contrastive step, 1/2/4/8 GPUs; MFMA % peak"
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/CU/clk (dense bf16, MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5033.2   # block-scaled f8f6f4 MFMA: 2x the bf16 rate (dense)
+PEAK_HBM_GBS = 8000.0      # HBM3E peak (MI355X_MICROARCH.md: 8 TB/s spec, ~6.3 achievable)
 
 
 def log(msg):
@@ -124,6 +125,14 @@ def algorithmic_bytes(cfg, B, train):
     out = {"gemm256_fwd_dgrad": sum((M * K + N * K + M * N) * 2 + x for M, N, K, x in fd) / len(fd)}
     if wg:
         out["gemm256_wgrad"] = sum(K * (M + N) * 2 + M * N * 4 for M, N, K in wg) / len(wg)
+    # attention (vision tower, one launch per layer and direction): forward reads Q, K, V and writes O
+    # (+ the fp32 row LSE); backward reads Q, K, V, O, dO and the LSE and writes dQ, dK, dV
+    v = cfg.vision_config
+    N = (v.image_size // v.patch_size) ** 2 + 1
+    T, D, H = B * N, v.hidden_size, v.num_attention_heads
+    fwd = T * 4 * D * 2 + B * H * N * 4
+    bwd = T * 8 * D * 2 + B * H * N * 4
+    out["attention"] = (fwd + bwd) / 2 if train else fwd
     return {k: round(v) for k, v in out.items()}
 
 
@@ -230,17 +239,27 @@ def family_roofline(name, launches, cfg, B, train):
     tot_fl = sum(f for _, f in launches)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
     peak = PEAK_FP8_TFLOPS if name == "gemm_fp8" else PEAK_BF16_TFLOPS
+    alg = algorithmic_bytes(cfg, B, train).get(name)
     res = {"bound": "mfma", "kernel": name, "labels": FAMILIES[name], "launches": len(launches),
            "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
            "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
            "frac": round(ach / peak, 4), "ms_per_step_caller_stream": None,
            "traffic": None, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": None,
-           "algorithmic_bytes": algorithmic_bytes(cfg, B, train).get(name)}
+           "algorithmic_bytes": alg}
+    if name == "attention" and alg:
+        # at CLIP's sequence lengths attention moves more bytes per FLOP than the chip's balance
+        # point (per token and head 4*N*64 FLOP against 4*64*2 B of Q, K, V, O: N/2 FLOP/B, 99 at
+        # N = 197, 289 at N = 577, vs 2.5 PF / 8 TB/s = 315), so its roofline is HBM: algorithmic
+        # bytes / mean launch time
+        gbs = alg / (tot_ms / len(launches) * 1e-3) / 1e9
+        res.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "mfma_tflops": round(ach, 1),
+                    "mfma_frac": round(ach / PEAK_BF16_TFLOPS, 4)})
     tf = TRAFFIC_FILES.get(name)
     if tf and os.path.isfile(os.path.join(REPO, tf)):
         try:
             tj = json.load(open(os.path.join(REPO, tf)))
-            if tj.get("kernel") == name and (tj.get("workload") in (None, f"{cfg.name}/{B}/{int(train)}")):
+            if tj.get("kernel") == name and tj.get("workload") == f"{cfg.name}/{B}/{int(train)}":
                 res["traffic"], res["traffic_source"] = tj["bytes_per_launch"], tf
         except (OSError, ValueError, KeyError):
             pass

@@ -15,6 +15,7 @@ FAMILIES = {
     "gemm256_fwd_dgrad": "gemm_pp_kernel",  # demangled or mangled names
 }
 PER_STEP, VISION, M_TILES = 97, 49, 788
+WORKLOAD = "ViT-B/16/1024/1"  # bench.py's default run (config name / per-GPU batch / training), matched by bench.py
 
 
 def per_dispatch(d, counter, kernel):
@@ -41,7 +42,7 @@ def summarize(family, fetch_dir, write_dir):
     write = vision_only(family, *per_dispatch(write_dir, "WRITE_SIZE", k))
     rd = 2.0 * 1024 * sum(fetch) / len(fetch)
     wr = 1024.0 * sum(write) / len(write)
-    return {"kernel": family, "launches": [len(fetch), len(write)], "read_bytes_per_launch": rd,
+    return {"kernel": family, "workload": WORKLOAD, "launches": [len(fetch), len(write)], "read_bytes_per_launch": rd,
             "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
             "subset": "vision tower launches (the ones bench.py's live roofline times on the caller's stream)",
             "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over CLIPMI_OVERLAP=0 bench.py "
