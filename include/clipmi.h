@@ -126,6 +126,13 @@ int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, 
  * to a multiple of 8 (the pad columns are zeroed: L/14's 588 -> 640); mean/std are 3 host floats. */
 int clipmi_im2col_u8(void* stream, int dtype, const uint8_t* images, void* X, int B, int Hin, int Win, int image_size,
                      int P, int Kp, const float* mean, const float* std);
+/* Input-step resize (dataset.py:152-164 -> CLIPImageProcessor, shortest edge = image size):
+ * PIL Image.resize(BICUBIC) of channels-last RGB uint8 [B, Hin, Win, 3] -> [B, Hout, Wout, 3],
+ * bit-exact (fp64 tap weights -> 22-bit fixed point, horizontal then vertical 8-bit pass; a pass
+ * whose size is unchanged is skipped).  Workspace: clipmi_resize_u8_ws bytes. */
+int64_t clipmi_resize_u8_ws(int B, int Hin, int Win, int Hout, int Wout);
+int clipmi_resize_u8(void* stream, const uint8_t* in, int B, int Hin, int Win, uint8_t* out, int Hout, int Wout,
+                     void* ws, int64_t ws_bytes);
 /* pooled token per row: mode 0 first token (model_m.py:102), 1 first EOS, 2 argmax id ([HF] :561-581) */
 int clipmi_pool_index(void* stream, const int64_t* ids, int B, int S, int64_t eos, int mode, int* idx);
 int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* out);

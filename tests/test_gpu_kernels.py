@@ -3,6 +3,8 @@ LayerNorm (+ fused vision embedding add), attention fwd/bwd (causal + key paddin
 bidirectional), embeddings, column sums, contrastive CE, AdamW and grad-norm."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -342,3 +344,27 @@ def test_attention_online_softmax_rescale(dtype, monkeypatch):
     oref, lref = attn_ref(qkv.float(), B, N, H, None, False)
     assert rel(o, oref) < TOL[dtype], "O"
     assert (lse - lref).abs().max().item() < (5e-2 if dtype == torch.bfloat16 else 1e-4), "lse"
+
+
+@pytest.mark.parametrize("tag", ["land", "port", "pair", "up", "wide"])
+def test_resize_u8_matches_processor(golden, tag):
+    """clipmi_resize_u8 = CLIPImageProcessor's (PIL bicubic) shortest-edge resize, bit-exact."""
+    from clipmi import towers as T
+    g = golden("image_processor_resize.npz")
+    imgs = torch.from_numpy(g[f"{tag}_images"]).cuda()
+    oh, ow = T.shortest_edge_size(imgs.shape[1], imgs.shape[2], 224)
+    out = T.resize_uint8(imgs, oh, ow)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), torch.from_numpy(g[f"{tag}_resized"]))
+
+
+def test_resize_u8_matches_oracle_random_sizes():
+    """Odd sizes in both directions, batch of 3, against the PIL restatement."""
+    from clipmi import towers as T
+    from oracle import resize_ref as RR
+    rng = np.random.default_rng(12)
+    for h, w, oh, ow in [(64, 80, 64, 71), (33, 47, 224, 300), (500, 40, 17, 230), (9, 9, 5, 3), (77, 77, 77, 50)]:
+        img = rng.integers(0, 256, (3, h, w, 3), dtype=np.uint8)
+        out = T.resize_uint8(torch.from_numpy(img).cuda(), oh, ow).cpu().numpy()
+        ref = np.stack([RR.resize_bicubic(im, oh, ow) for im in img])
+        assert np.array_equal(out, ref), (h, w, oh, ow)

@@ -142,16 +142,20 @@ def test_training_reduces_loss_bf16():
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_uint8_images_match_processor_path(precision):
-    """uint8 channels-last images through the fused input step give the logits of the
-    reference's path (CLIPImageProcessor pixel_values; oracle.image_processor, pinned by
-    tests/golden/image_processor.npz) on the same model and captions."""
+    """uint8 channels-last images through the GPU input step (shortest-edge resize, center crop,
+    rescale, normalize) give the logits of the reference's path (CLIPImageProcessor
+    pixel_values; oracle resize_ref + image_processor, pinned by tests/golden/image_processor*.npz)
+    on the same model and captions."""
     from oracle import clip_ref as R
+    from oracle import resize_ref as RR
     from clipmi import towers as T
     m = make("tiny", False, precision, freeze=True)
     cfg = m.config
     rng = np.random.default_rng(5)
     imgs = rng.integers(0, 256, (2, 72, 80, 3), dtype=np.uint8)
-    pv = R.image_processor(imgs, cfg.vision_config.image_size, T.IMAGE_MEAN, T.IMAGE_STD)
+    S = cfg.vision_config.image_size
+    oh, ow = RR.shortest_edge_size(72, 80, S)
+    pv = R.image_processor(np.stack([RR.resize_bicubic(im, oh, ow) for im in imgs]), S, T.IMAGE_MEAN, T.IMAGE_STD)
     b = batch(cfg, 2)
     with torch.no_grad():
         a = m(input_ids=b["input_ids"], attention_mask=b["attention_mask"], pixel_values=torch.from_numpy(pv).cuda())
@@ -508,3 +512,18 @@ def test_enhanced_adapter_main_checkpoint_roundtrip(tmp_path):
             assert torch.equal(getattr(b, name).state_dict()[k], v)
     with pytest.raises(FileNotFoundError):
         b.load_adapter_weights(str(tmp_path / "missing.pth"))
+
+
+@pytest.mark.parametrize("tag", ["pair", "land"])
+def test_uint8_images_match_processor_b32(golden, tag):
+    """B/32 (224 px) on raw uint8 images vs the reference processor's own pixel_values
+    (CLIPImageProcessor with resize, tests/golden/image_processor_resize.npz)."""
+    g = golden("image_processor_resize.npz")
+    m = CLIPWithAdapters("B/32", use_shared_adapters=False, device="cuda", precision="fp32")
+    n = g[f"{tag}_images"].shape[0]
+    b = batch(m.config, n)
+    with torch.no_grad():
+        a = m.get_image_features(torch.from_numpy(g[f"{tag}_pixel_values"]).cuda())
+        u = m.get_image_features(torch.from_numpy(g[f"{tag}_images"]).cuda())
+    torch.cuda.synchronize()
+    assert (a - u).abs().max().item() < 1e-4 * max(1.0, a.abs().max().item())

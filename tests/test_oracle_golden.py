@@ -270,3 +270,28 @@ def test_reference_checkpoint_forward(golden):
         out = R.clip_with_adapters_forward(batch(cfg, 2, g), p, cfg, ta, va)
     for k in ("logits_per_text", "text_features", "image_features"):
         np.testing.assert_allclose(out[k].numpy(), g[k], atol=2e-5, rtol=1e-4, err_msg=k)
+
+
+@pytest.mark.parametrize("tag", ["land", "port", "pair", "up", "wide"])
+def test_resize_oracle_matches_processor(golden, tag):
+    """oracle.resize_ref (PIL bicubic restated) = CLIPImageProcessor's resize bit for bit, and with
+    center crop + rescale + normalize its pixel_values (tests/golden/image_processor_resize.npz)."""
+    from oracle import resize_ref as RR
+    g = golden("image_processor_resize.npz")
+    imgs = g[f"{tag}_images"]
+    oh, ow = RR.shortest_edge_size(imgs.shape[1], imgs.shape[2], 224)
+    rs = np.stack([RR.resize_bicubic(im, oh, ow) for im in imgs])
+    assert np.array_equal(rs, g[f"{tag}_resized"])
+    pv = R.image_processor(rs, 224, [0.48145466, 0.4578275, 0.40821073], [0.26862954, 0.26130258, 0.27577711])
+    np.testing.assert_allclose(pv, g[f"{tag}_pixel_values"], atol=1e-6)
+
+
+def test_resize_oracle_matches_pil():
+    """The restatement against PIL itself (Pillow, the processor's backend) on random sizes."""
+    from PIL import Image
+    from oracle import resize_ref as RR
+    rng = np.random.default_rng(11)
+    for h, w, oh, ow in [(64, 80, 64, 71), (33, 47, 224, 300), (500, 40, 17, 230), (256, 256, 224, 224), (9, 9, 5, 3)]:
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        ref = np.asarray(Image.fromarray(img).resize((ow, oh), resample=Image.BICUBIC))
+        assert np.array_equal(RR.resize_bicubic(img, oh, ow), ref), (h, w, oh, ow)

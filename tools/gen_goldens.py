@@ -463,6 +463,29 @@ def gen_image_processor():
     save("image_processor.npz", **out)
 
 
+def gen_image_processor_resize():
+    """The full input step with resize: transformers' CLIPImageProcessor with OpenAI defaults
+    (shortest edge 224, PIL bicubic, center crop 224, rescale, normalize) on uint8 batches of
+    several sizes (down- and up-scaling, both orientations), plus the resized uint8 images alone
+    (do_center_crop / do_rescale / do_normalize off) to pin the resize bit-exactly."""
+    from transformers import CLIPImageProcessor
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        proc = CLIPImageProcessor()
+    rng = np.random.default_rng(2025)
+    out = {}
+    for tag, (b, h, w) in (("land", (1, 300, 400)), ("port", (1, 500, 333)), ("pair", (2, 240, 256)),
+                           ("up", (1, 150, 200)), ("wide", (1, 97, 700))):
+        img = rng.integers(0, 256, (b, h, w, 3), dtype=np.uint8)
+        out[f"{tag}_images"] = img
+        out[f"{tag}_pixel_values"] = proc(images=list(img), return_tensors="np")["pixel_values"]
+        out[f"{tag}_resized"] = np.stack([proc(images=[im], return_tensors="np", do_center_crop=False, do_rescale=False,
+                                               do_normalize=False)["pixel_values"][0].transpose(1, 2, 0)
+                                          for im in img]).astype(np.uint8)
+    save("image_processor_resize.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     if len(sys.argv) > 1:  # named generators only

@@ -85,14 +85,38 @@ IMAGE_STD = (0.26862954, 0.26130258, 0.27577711)
 
 
 def im2col_uint8(images, X, image_size, patch, mean=IMAGE_MEAN, std=IMAGE_STD):
-    """uint8 images [B, H, W, 3] (channels last, H, W >= image_size) -> normalised im2col rows
-    in X [B*(G*G+1), 3*P*P]: CLIPImageProcessor's center_crop + rescale + normalize fused into
-    patch-embed's im2col (one kernel, 1 B read per pixel value instead of 4)."""
+    """uint8 images [B, H, W, 3] (channels last, H, W >= image_size: resized by resize_uint8
+    first) -> normalised im2col rows in X [B*(G*G+1), 3*P*P]: CLIPImageProcessor's center_crop +
+    rescale + normalize fused into patch-embed's im2col (one kernel, 1 B read per pixel value
+    instead of 4)."""
     B, H, W, C = images.shape
     m = (c_float * 3)(*mean)
     sd = (c_float * 3)(*std)
     call("clipmi_im2col_u8", K.stream(), dcode(X.dtype), P_(images), P_(X), B, H, W, image_size, patch,
          X.shape[1], m, sd)
+_lib.declare("clipmi_resize_u8_ws", [c_int, c_int, c_int, c_int, c_int], c_i64)
+_lib.declare("clipmi_resize_u8", [c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_i64])
+
+
+def shortest_edge_size(h, w, size):
+    """CLIPImageProcessor's output size (transformers get_resize_output_image_size,
+    default_to_square=False): short edge -> size, long edge -> int(size * long / short)."""
+    if w <= h:
+        return int(size * h / w), size
+    return size, int(size * w / h)
+
+
+def resize_uint8(images, out_h, out_w):
+    """CLIPImageProcessor's resize of uint8 [B, H, W, 3] (PIL bicubic, bit-exact) on the GPU
+    (clipmi_resize_u8)."""
+    B, H, W, C = images.shape
+    out = torch.empty(B, out_h, out_w, C, dtype=torch.uint8, device=images.device)
+    nb = int(_lib.lib().clipmi_resize_u8_ws(B, H, W, out_h, out_w))
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=images.device)
+    call("clipmi_resize_u8", K.stream(), P_(images), B, H, W, P_(out), out_h, out_w, P_(ws), nb)
+    return out
+
+
 _lib.declare("clipmi_pool_index", [c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp])
 _lib.declare("clipmi_gather_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp])
 _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int])
@@ -301,8 +325,6 @@ class VisionTowerFn(torch.autograd.Function):
             if pixel_values.dim() != 4 or pixel_values.shape[3] != v.num_channels:
                 raise ValueError(f"uint8 images must be [B, H, W, {v.num_channels}] (channels last)")
             H, W = pixel_values.shape[1], pixel_values.shape[2]
-            if H < v.image_size or W < v.image_size:
-                raise ValueError(f"uint8 images ({H}*{W}) are smaller than the crop ({v.image_size}); resize first")
         else:
             if pixel_values.dim() != 4 or pixel_values.shape[1] != v.num_channels:
                 raise ValueError(f"pixel_values must be [B, {v.num_channels}, H, W]")
@@ -311,6 +333,11 @@ class VisionTowerFn(torch.autograd.Function):
                 raise ValueError(f"Input image size ({H}*{W}) doesn't match model ({v.image_size}*{v.image_size}).")
         dev = pixel_values.device
         px = pixel_values.contiguous() if raw else pixel_values.to(torch.float32).contiguous()
+        if raw:  # CLIPImageProcessor: resize the shortest edge to the image size, then center-crop
+            oh, ow = shortest_edge_size(H, W, v.image_size)
+            if (oh, ow) != (H, W):
+                px = resize_uint8(px, oh, ow)
+                H, W = oh, ow
         N, D, Pp = v.num_positions, v.hidden_size, v.patch_size
         Kc = v.num_channels * Pp * Pp
         # patch K padded to a multiple of 64 (ViT-L/14: 588 -> 640) so both GEMM operands are

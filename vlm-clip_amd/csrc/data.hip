@@ -8,6 +8,7 @@
 // takes the first EOS (or argmax id when eos_token_id == 2).
 #include "common.h"
 #include "internal.h"
+#include <cmath>
 
 namespace {
 
@@ -142,6 +143,94 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const T* src, const i
   }
 }
 
+// ---- input-step resize: CLIPImageProcessor's shortest-edge resize = PIL Image.resize(BICUBIC)
+// (transformers CLIPImageProcessorPil; PIL libImaging/Resample.c, restated in oracle/resize_ref.py
+// and bit-exact against PIL): per output coordinate the taps [xmin, xmin + n) and fp64 bicubic
+// (a = -0.5) weights stretched by max(in/out, 1), normalised, then fixed point with 22 fraction
+// bits; a horizontal 8-bit pass, then a vertical one, each out = clamp((2^21 + sum k*in) >> 22).
+// Tables: per output coordinate [xmin, n, k_0 .. k_{ksize-1}] int32.
+constexpr int RS_PREC = 22;
+
+__device__ double rs_bicubic(double x) {
+#pragma clang fp contract(off)
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1.0;
+  if (x < 2.0) return (((x - 5.0) * x + 8.0) * x - 4.0) * a;
+  return 0.0;
+}
+
+// one thread per output coordinate; fp64 exactly as PIL's precompute_coeffs (no contraction)
+__global__ void resize_coeffs_kernel(int in_size, int out_size, int ksize, int* tab) {
+#pragma clang fp contract(off)
+  const int xx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (xx >= out_size) return;
+  const double scale = (double)in_size / (double)out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 2.0 * filterscale;
+  const double ss = 1.0 / filterscale;
+  const double center = (xx + 0.5) * scale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  xmax -= xmin;
+  int* t = tab + (int64_t)xx * (2 + ksize);
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) ww += rs_bicubic((x + xmin - center + 0.5) * ss);
+  for (int x = 0; x < ksize; ++x) {
+    int k = 0;
+    if (x < xmax) {
+      double w = rs_bicubic((x + xmin - center + 0.5) * ss);
+      if (ww != 0.0) w /= ww;
+      k = w < 0 ? (int)(-0.5 + w * (double)(1 << RS_PREC)) : (int)(0.5 + w * (double)(1 << RS_PREC));
+    }
+    t[2 + x] = k;
+  }
+  t[0] = xmin;
+  t[1] = xmax;
+}
+
+__device__ __forceinline__ uint8_t rs_clip8(int acc) {
+  const int v = acc >> RS_PREC;
+  return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+}
+
+// horizontal (HORIZ) or vertical pass over channels-last RGB: one thread per output pixel
+template <bool HORIZ>
+__global__ __launch_bounds__(256) void resize_pass_kernel(const uint8_t* in, uint8_t* out, int B, int Hin, int Win,
+                                                          int Hout, int Wout, const int* tab, int ksize) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)B * Hout * Wout;
+  if (i >= total) return;
+  const int xo = (int)(i % Wout);
+  const int64_t r = i / Wout;
+  const int yo = (int)(r % Hout), b = (int)(r / Hout);
+  const int* t = tab + (int64_t)(HORIZ ? xo : yo) * (2 + ksize);
+  const int lo = t[0], n = t[1];
+  int a0 = 1 << (RS_PREC - 1), a1 = a0, a2 = a0;
+  const uint8_t* src = HORIZ ? in + (((int64_t)b * Hin + yo) * Win + lo) * 3 : in + (((int64_t)b * Hin + lo) * Win + xo) * 3;
+  const int64_t step = HORIZ ? 3 : (int64_t)Win * 3;
+  for (int j = 0; j < n; ++j) {
+    const int k = t[2 + j];
+    a0 += k * (int)src[0];
+    a1 += k * (int)src[1];
+    a2 += k * (int)src[2];
+    src += step;
+  }
+  uint8_t* dst = out + i * 3;
+  dst[0] = rs_clip8(a0);
+  dst[1] = rs_clip8(a1);
+  dst[2] = rs_clip8(a2);
+}
+
+int rs_ksize(int in, int out) {
+  const double scale = (double)in / (double)out;
+  const double support = 2.0 * (scale < 1.0 ? 1.0 : scale);
+  return (int)ceil(support) * 2 + 1;
+}
+int64_t rs_al(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
 }  // namespace
 
 extern "C" int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, int C, int H, int P, int Kp) {
@@ -209,6 +298,44 @@ extern "C" int clipmi_gather_rows(void* stream, int dtype, const void* src, cons
 extern "C" int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* dst, int beta) {
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(scatter_rows_kernel<bf16>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, idx, B, S, D, (bf16*)dst, beta);
   else hipLaunchKernelGGL(scatter_rows_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const float*)src, idx, B, S, D, (float*)dst, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// ---- input-step resize (see resize_pass_kernel): workspace = the two coefficient tables + the
+// horizontally resized intermediate [B, Hin, Wout, 3]
+extern "C" int64_t clipmi_resize_u8_ws(int B, int Hin, int Win, int Hout, int Wout) {
+  return rs_al((int64_t)Wout * (2 + rs_ksize(Win, Wout)) * 4) + rs_al((int64_t)Hout * (2 + rs_ksize(Hin, Hout)) * 4) +
+         rs_al((int64_t)B * Hin * Wout * 3);
+}
+
+extern "C" int clipmi_resize_u8(void* stream, const uint8_t* in, int B, int Hin, int Win, uint8_t* out, int Hout,
+                                int Wout, void* ws, int64_t ws_bytes) {
+  CLIPMI_REQUIRE(B >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0, "resize: sizes");
+  CLIPMI_REQUIRE(ws && ws_bytes >= clipmi_resize_u8_ws(B, Hin, Win, Hout, Wout), "resize: workspace too small");
+  if (B == 0) return CLIPMI_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int kw = rs_ksize(Win, Wout), kh = rs_ksize(Hin, Hout);
+  int* htab = (int*)ws;
+  int* vtab = (int*)((char*)ws + rs_al((int64_t)Wout * (2 + kw) * 4));
+  uint8_t* tmp = (uint8_t*)vtab + rs_al((int64_t)Hout * (2 + kh) * 4);
+  const bool hz = Wout != Win, vt = Hout != Hin;  // PIL skips a pass whose size does not change
+  if (!hz && !vt) {
+    CLIPMI_HIP(hipMemcpyAsync(out, in, (size_t)B * Hin * Win * 3, hipMemcpyDeviceToDevice, s));
+    return CLIPMI_OK;
+  }
+  if (hz) {
+    hipLaunchKernelGGL(resize_coeffs_kernel, dim3((Wout + 255) / 256), dim3(256), 0, s, Win, Wout, kw, htab);
+    const int64_t n = (int64_t)B * Hin * Wout;
+    hipLaunchKernelGGL(resize_pass_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in,
+                       vt ? tmp : out, B, Hin, Win, Hin, Wout, htab, kw);
+  }
+  if (vt) {
+    hipLaunchKernelGGL(resize_coeffs_kernel, dim3((Hout + 255) / 256), dim3(256), 0, s, Hin, Hout, kh, vtab);
+    const int64_t n = (int64_t)B * Hout * Wout;
+    hipLaunchKernelGGL(resize_pass_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       hz ? tmp : in, out, B, Hin, Wout, Hout, Wout, vtab, kh);
+  }
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
