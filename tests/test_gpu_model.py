@@ -527,3 +527,29 @@ def test_uint8_images_match_processor_b32(golden, tag):
         u = m.get_image_features(torch.from_numpy(g[f"{tag}_images"]).cuda())
     torch.cuda.synchronize()
     assert (a - u).abs().max().item() < 1e-4 * max(1.0, a.abs().max().item())
+
+
+def test_config3_full_size_overlap_is_bitwise_serial(monkeypatch):
+    """Config 3 at its full size (B/16 full fine-tune, B = 1024, bf16): running the text tower
+    on its own stream beside the vision tower (the benchmarked schedule) must not change a bit of
+    the loss or of any non-atomic gradient versus the serial schedule; a race between the two
+    streams' kernels or workspaces would show here and not at test sizes."""
+    res = {}
+    for ov in ("0", "1"):
+        monkeypatch.setenv("CLIPMI_OVERLAP", ov)
+        m = CLIPWithAdapters("B/16", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                             freeze_clip=False, device="cuda", precision="bf16", fast_init=True)
+        b = batch(m.config, 1024)
+        out = m(**b, return_loss=True)
+        out["loss"].backward()
+        torch.cuda.synchronize()
+        assert torch.isfinite(out["loss"]).item()
+        res[ov] = (out["loss"].detach().clone(),
+                   {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+        del m, out, b
+        torch.cuda.empty_cache()
+    (l0, g0), (l1, g1) = res["0"], res["1"]
+    assert torch.equal(l0, l1)
+    racy = [n for n in g0 if not torch.equal(g0[n], g1[n]) and not any(k in n for k in _ATOMIC_GRADS)]
+    print(f"\n[config 3 full size] loss {l0.item():.5f}; {len(g0)} gradients, differing beyond atomics: {racy[:6]}")
+    assert not racy
