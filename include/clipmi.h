@@ -36,7 +36,8 @@ const char* clipmi_last_error(void);
  *        bit4 *= quick_gelu'(aux[m,n]) | bit5 *= gelu_erf'(aux[m,n])
  *        bit6 C += result (beta = 1) | bit7 store pre-activation to aux[m,n]
  * dtypes: A/B bf16 (MFMA path) or f32 (exact-f32 parity path); C/residual/aux in c_dtype.
- * split_k > 1 (fp32 C, beta flag only) uses workspace of split_k*M*N floats.
+ * split_k > 1 (fp32 C, beta flag only) uses workspace of split_k*M*N floats (+ split_k*M with
+ * bias_grad: per-split bias partials summed in split order, so results are run-to-run identical).
  */
 typedef struct clipmi_gemm_desc {
   int M, N, K;

@@ -107,17 +107,23 @@ def test_gemm_splitk_wgrad(dtype):
 @pytest.mark.parametrize("T,Nout,Kin,split", [(3000, 256, 192, 8), (50000, 768, 3072, 12), (77, 64, 128, 1),
                                               (20000, 2304, 768, 4), (300, 768, 768, 3), (4100, 512, 256, 2)])
 def test_wgrad_fused_bias_grad(T, Nout, Kin, split):
-    """256 wgrad kernel with the fused bias gradient (sum over tokens of dY)."""
+    """256 wgrad kernel with the fused bias gradient (sum over tokens of dY); split-K bias partials
+    are summed in split order, so a second run gives bitwise the same bias gradient."""
     dY = _mk((T, Nout), torch.bfloat16, 12)
     X = _mk((T, Kin), torch.bfloat16, 13)
     C = _mk((Nout, Kin), torch.float32, 14)
     db = _mk((Nout,), torch.float32, 15)
     c0, db0 = C.clone(), db.clone()
-    ws = torch.empty(max(1, split) * Nout * Kin, device="cuda", dtype=torch.float32)
+    ws = torch.empty(max(1, split) * Nout * (Kin + 1), device="cuda", dtype=torch.float32)  # + bias partials
     kern.gemm(Nout, Kin, T, dY, Nout, False, X, Kin, False, C, Kin, flags=_lib.EPI_BETA, split_k=split,
               workspace=ws, bias_grad=db)
     ref = c0 + dY.float().t() @ X.float()
     dref = db0 + dY.float().sum(0)
+    db2 = db0.clone()
+    kern.gemm(Nout, Kin, T, dY, Nout, False, X, Kin, False, C.clone(), Kin, flags=_lib.EPI_BETA, split_k=split,
+              workspace=ws, bias_grad=db2)
+    torch.cuda.synchronize()
+    assert torch.equal(db2, db)
     torch.cuda.synchronize()
     assert (C - ref).abs().max().item() / ref.abs().max().item() < 1e-2
     assert (db - dref).abs().max().item() / dref.abs().max().item() < 1e-3

@@ -81,7 +81,7 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
                 split, best = sp, score
     if split == 0:
         continue
-    ws = torch.empty(split * M * N, device="cuda") if split > 1 else None
+    ws = torch.empty(split * M * (N + 1), device="cuda") if split > 1 else None  # slabs + bias partials
     bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,
               split_k=split, workspace=ws, bias_grad=bg)

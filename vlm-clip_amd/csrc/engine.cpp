@@ -123,7 +123,7 @@ WsPlan plan(const clipmi_encoder_desc* d) {
   const int shapes[4][2] = {{d->F, d->D}, {d->D, d->F}, {d->D, d->D}, {3 * d->D, d->D}};
   for (auto& sh : shapes) {
     const int s = wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
-    if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * sh[1] * 4);
+    if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * (sh[1] + 1) * 4);  // slabs + bias partials
   }
   p.colsum = p.split + align256(sp);
   p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));

@@ -52,6 +52,7 @@ struct GemmP {
   const uint8_t* a_scale; const uint8_t* b_scale;  // MXFP8: E8M0 per 32-element k-block, [rows][K/32]
   uint8_t* c_scale;                                 // MXFP8 output: E8M0 per 32 columns, [M][N/32]
   int raster;  // 0: tiles row-major; g > 0: g tile-rows at a time, column by column (tile_coords)
+  float* bws;  // split-K with a fused bias gradient: per-split partial sums [splits][M] (no atomics)
 };
 
 // tile -> (tm, tn).  Row-major, or grouped: g tile-rows at a time, walked column by column, so
@@ -772,7 +773,10 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmP p, float* bias_gr
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + wm * 128 + i * 16 + lane;
-      if (m < p.M) atomicAdd(bias_grad + m, accb[i][0]);
+      if (m < p.M) {
+        if (p.bws) p.bws[(int64_t)kz * p.M + m] = accb[i][0];  // summed in split order afterwards
+        else atomicAdd(bias_grad + m, accb[i][0]);             // one split: one add per element
+      }
     }
   }
   finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, kz);
@@ -967,7 +971,10 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
       const int m = m0 + wm * 128 + (mh * 4 + wn) * 16 + lane;
-      if (m < p.M) atomicAdd(bias_grad + m, accb[mh][0]);
+      if (m < p.M) {
+        if (p.bws) p.bws[(int64_t)kz * p.M + m] = accb[mh][0];  // summed in split order afterwards
+        else atomicAdd(bias_grad + m, accb[mh][0]);              // one split: one add per element
+      }
     }
   }
   if constexpr (PPV & 8) {  // timing experiment: main loop only, results kept live, nothing stored
@@ -1658,6 +1665,16 @@ __global__ void splitk_reduce_kernel(const float* ws, float* C, int64_t ldc, int
 
 // same reduction, four columns per lane and eight slabs' loads in flight before the (fixed-order)
 // adds: the scalar loop above waits one HBM round trip per slab.  N % 4 == 0, ldc % 4 == 0.
+// bias_grad[m] += sum over splits of the per-split partials, in split order (deterministic)
+__global__ __launch_bounds__(256) void bias_partials_reduce_kernel(const float* bws, float* bias_grad, int M,
+                                                                   int splits) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float acc = 0.f;
+  for (int z = 0; z < splits; ++z) acc += bws[(int64_t)z * M + m];
+  bias_grad[m] += acc;
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* ws, float* C, int64_t ldc, int M, int N,
                                                              int splits, float alpha, int beta) {
   const int64_t total = (int64_t)M * N;
@@ -1923,6 +1940,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.aux = d->aux; p.ldaux = d->ldaux; p.alpha = d->alpha; p.flags = d->flags;
   p.bias_f32 = d->bias_dtype == CLIPMI_F32;
   p.ws = nullptr;
+  p.bws = nullptr;
   // 256-kernel schedule: the ping-pong kernel for the forward / dgrad layouts, the
   // single-group asm-DMA schedule (var 4) for wgrad, where its 64-k steps measured faster
   // (profiles/r01_gemm_variants*.log).  CLIPMI_GEMM_VAR overrides it for A/B runs.
@@ -1961,12 +1979,14 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   if (splits > 1) {
     CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32, "split_k needs fp32 C");
     CLIPMI_REQUIRE((d->flags & ~CLIPMI_EPI_BETA) == 0, "split_k supports only the beta flag");
-    CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4, "split_k workspace too small");
+    CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= (int64_t)splits * d->M * (d->N + (d->bias_grad ? 1 : 0)) * 4,
+                   "split_k workspace too small (split_k * M * (N + bias_grad ? 1 : 0) floats)");
     int per = (d->K + splits - 1) / splits;
     per = (per + kstep - 1) / kstep * kstep;
     splits = (d->K + per - 1) / per;
     p.k_per_split = per;
     p.ws = (float*)d->workspace;
+    if (d->bias_grad) p.bws = p.ws + (int64_t)splits * d->M * d->N;
   } else {
     p.k_per_split = d->K > 0 ? d->K : 1;
   }
@@ -2014,6 +2034,9 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
                          p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta);
     }
+    if (p.bws)
+      hipLaunchKernelGGL(bias_partials_reduce_kernel, dim3((d->M + 255) / 256), dim3(256), 0, s, p.bws, d->bias_grad,
+                         d->M, splits);
     CLIPMI_CHECK_LAUNCH();
   }
   return CLIPMI_OK;
