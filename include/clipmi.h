@@ -194,6 +194,17 @@ int clipmi_contrastive_ce_fwd(void* stream, const float* S, float* logits, const
 /* dS = g*exp(ls)*(softmax - onehot)*norm ; dls_row = sum_j dlogit*logit */
 int clipmi_contrastive_ce_bwd(void* stream, const float* logits, const float* lse, const float* logit_scale,
                               const float* grad_out, int B, int Bg, int label0, float norm, float* dS, float* dls_row);
+/* Column-streamed form (the [B, Bg] blocks never materialised): the caller walks chunks
+ * [col0, col0 + C) of the cosine block S (row stride C).  fwd_chunk merges the chunk into the
+ * running per-row (max, sum-of-exp) pairs run [B][2] (col0 == 0 initialises them) and stores
+ * the label logit lab[i] when column label0 + i lies in the chunk; finish turns them into lse, ce.
+ * bwd_chunk writes the chunk's dS [B][C] and sets (beta = 0) or accumulates dls_row. */
+int clipmi_contrastive_ce_fwd_chunk(void* stream, const float* S, const float* logit_scale, int B, int C, int col0,
+                                    int Bg, int label0, float* run, float* lab);
+int clipmi_contrastive_ce_finish(void* stream, const float* run, const float* lab, int B, float* lse, float* ce);
+int clipmi_contrastive_ce_bwd_chunk(void* stream, const float* S, const float* lse, const float* logit_scale,
+                                    const float* grad_out, int B, int C, int col0, int Bg, int label0, float norm,
+                                    float* dS, float* dls_row, int beta);
 int clipmi_sum2(void* stream, const float* a, const float* b, int n, float scale, float* out, int beta);
 
 /* ---- Optimizer (trainer.py:95,98; [HF] optimization.py:101-129) ------------------------------ */

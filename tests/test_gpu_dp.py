@@ -13,8 +13,10 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q, overlap=False):
+def _worker(rank, world, port, q, overlap=False, chunk=None):
     import sys
+    if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
+        os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
     sys.path.insert(0, os.path.join(REPO, "vlm-clip_amd"))
     import torch.distributed as dist
     from clipmi import CLIPWithAdapters, synth
@@ -43,15 +45,15 @@ def _worker(rank, world, port, q, overlap=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_two_rank_data_parallel_matches_single_device(overlap):
+@pytest.mark.parametrize("overlap,chunk", [(False, None), (True, None), (False, 3)])
+def test_two_rank_data_parallel_matches_single_device(overlap, chunk):
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500
-    port += 37 * int(overlap)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
+    port += 37 * int(overlap) + 71 * int(chunk is not None)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])

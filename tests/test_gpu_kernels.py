@@ -237,6 +237,42 @@ def test_contrastive_fn_matches_torch(B, E):
     assert abs(ar.grad[0].item() - lr_.grad.item()) < 1e-4 * max(1, abs(lr_.grad.item()))
 
 
+@pytest.mark.parametrize("B,E,chunk", [(1000, 512, 256), (1000, 512, 333), (4096, 768, 1024), (64, 64, 1)])
+def test_contrastive_streamed_matches_materialised(B, E, chunk, monkeypatch):
+    """Column-streamed InfoNCE (Bg > CLIPMI_CE_CHUNK: online log-sum-exp over column chunks,
+    chunk recompute in backward, [B, Bg] never materialised) against the plain path."""
+
+    class _A:
+        def __init__(self):
+            self.grad = torch.zeros(64, device="cuda")
+
+        def prepare_grads(self):
+            pass
+
+        def ptr(self, name, buf):
+            return buf.data_ptr()
+
+    res = []
+    for ch in (None, chunk):
+        if ch is None:
+            monkeypatch.delenv("CLIPMI_CE_CHUNK", raising=False)
+        else:
+            monkeypatch.setenv("CLIPMI_CE_CHUNK", str(ch))
+        t = rnd((B, E), 26).requires_grad_(True)
+        i = rnd((B, E), 27).requires_grad_(True)
+        ls = torch.tensor(math.log(100.0), device="cuda", requires_grad=True)
+        ar = _A()
+        loss, th, ih, lt, li = T.ContrastiveFn.apply(t, i, ls, None, True, ar)
+        assert (lt is None) == (ch is not None)
+        (loss + (th * th.detach()).sum() * 1e-3).backward()  # a feature-output gradient too
+        res.append((loss.item(), t.grad, i.grad, ar.grad[0].item()))
+    (l0, t0, i0, s0), (l1, t1, i1, s1) = res
+    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
+    assert rel(t1, t0) < 1e-5
+    assert rel(i1, i0) < 1e-5
+    assert abs(s1 - s0) < 1e-5 * max(1.0, abs(s0))
+
+
 def test_adamw_and_clip_match_torch():
     n = 100_003
     p = rnd((n,), 24)

@@ -299,7 +299,7 @@ class CLIPWithAdapters(nn.Module):
                                                          group, True, self.clip.arena)
             world = torch.distributed.get_world_size(group) if group is not None else 1
             return {"loss": loss, "text_features": t, "image_features": i, "logits_per_text": lpt,
-                    "logits_per_image": lpt.t() if world == 1 else lpi}
+                    "logits_per_image": lpt.t() if world == 1 and lpt is not None else lpi}
         return {"text_features": text_features, "image_features": image_features}
 
     def _both_towers_overlapped(self, input_ids, attention_mask, pixel_values):

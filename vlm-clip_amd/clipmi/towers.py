@@ -18,6 +18,7 @@ Reference mapping:
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -128,6 +129,10 @@ _lib.declare("clipmi_l2norm_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int])
 _lib.declare("clipmi_contrastive_ce_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp])
 _lib.declare("clipmi_contrastive_ce_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp])
 _lib.declare("clipmi_sum2", [c_vp, c_vp, c_vp, c_int, c_float, c_vp, c_int])
+_lib.declare("clipmi_contrastive_ce_fwd_chunk", [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp])
+_lib.declare("clipmi_contrastive_ce_finish", [c_vp, c_vp, c_vp, c_int, c_vp, c_vp])
+_lib.declare("clipmi_contrastive_ce_bwd_chunk", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                                 c_float, c_vp, c_vp, c_int])
 _lib.declare("clipmi_cast_f32_bf16", [c_vp, c_vp, c_vp, c_i64])
 _lib.declare("clipmi_grad_norm_ws", [], c_i64)
 _lib.declare("clipmi_grad_norm", [c_vp, c_vp, c_i64, c_float, c_vp, c_vp, c_i64])
@@ -697,11 +702,54 @@ def _reduce_scatter(x, group, world):
     return y[r * n:(r + 1) * n].contiguous()
 
 
+def contrastive_chunk():
+    """Columns per chunk of the column-streamed contrastive (CLIPMI_CE_CHUNK, default 8192): a
+    global batch wider than this is never materialised as [B, Bg] blocks (BASELINE config 5:
+    Bg = 32768 at B = 4096 per GPU would be four 512 MiB fp32 blocks); at config 3 (Bg <= 8192)
+    the whole block is one chunk and the plain path runs."""
+    return max(1, int(os.environ.get("CLIPMI_CE_CHUNK", "8192")))
+
+
+def _ce_streamed_fwd(s, x_local, y_all, ls, lab0, C, lse, ce):
+    """Row-wise CE of logits = exp(ls) * x_local y_all^T over column chunks of width C."""
+    B, E = x_local.shape
+    Bg = y_all.shape[0]
+    dev = x_local.device
+    sbuf = torch.empty(B * min(C, Bg), dtype=torch.float32, device=dev)
+    run = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    lab = torch.empty(B, dtype=torch.float32, device=dev)
+    for c0 in range(0, Bg, C):
+        cw = min(C, Bg - c0)
+        _gemm_f32(B, cw, E, x_local, E, True, y_all[c0:], E, True, sbuf, cw)
+        call("clipmi_contrastive_ce_fwd_chunk", s, P_(sbuf), P_(ls), B, cw, c0, Bg, lab0, P_(run), P_(lab))
+    call("clipmi_contrastive_ce_finish", s, P_(run), P_(lab), B, P_(lse), P_(ce))
+
+
+def _ce_streamed_bwd(s, x_local, y_all, ls, gl, lse, lab0, norm, C, dls, dy_all, dx_local):
+    """Gradients of the streamed CE: dy_all[j] = sum_i dS[i, j] x_local[i] (column direction,
+    every chunk writes its own rows) and dx_local = sum_j dS[:, j] y_all[j] (row direction,
+    accumulated over the chunks), recomputing each chunk's cosines."""
+    B, E = x_local.shape
+    Bg = y_all.shape[0]
+    dev = x_local.device
+    sbuf = torch.empty(B * min(C, Bg), dtype=torch.float32, device=dev)
+    dbuf = torch.empty_like(sbuf)
+    for n, c0 in enumerate(range(0, Bg, C)):
+        cw = min(C, Bg - c0)
+        _gemm_f32(B, cw, E, x_local, E, True, y_all[c0:], E, True, sbuf, cw)
+        call("clipmi_contrastive_ce_bwd_chunk", s, P_(sbuf), P_(lse), P_(ls), P_(gl), B, cw, c0, Bg, lab0, norm,
+             P_(dbuf), P_(dls), 1 if n else 0)
+        _gemm_f32(cw, E, B, dbuf, cw, False, x_local, E, False, dy_all[c0:], E)
+        _gemm_f32(B, E, cw, dbuf, cw, True, y_all[c0:], E, False, dx_local, E, flags=_lib.EPI_BETA if n else 0)
+
+
 class ContrastiveFn(torch.autograd.Function):
     """Symmetric InfoNCE.  Single device: exactly model_m.py:146-171.  With a process group
     of W ranks: all-gather the normalised features, each rank scores its B rows
     against all Bg = W*B columns with label offset rank*B, loss normalised by 2*Bg (so the
-    all-reduced sum is the global loss), feature gradients reduce-scattered back."""
+    all-reduced sum is the global loss), feature gradients reduce-scattered back.  When Bg
+    exceeds contrastive_chunk() the score blocks are streamed by column chunks (online
+    log-sum-exp forward, chunk recompute backward) and the logits outputs are None."""
 
     @staticmethod
     def forward(ctx, tf, imf, logit_scale, group, global_loss, arena):
@@ -719,14 +767,31 @@ class ContrastiveFn(torch.autograd.Function):
         call("clipmi_l2norm_fwd", s, P_(i), P_(ih), P_(inn), B, E)
         tg, ig = _gather(th, group, world), _gather(ih, group, world)
         Bg = tg.shape[0]
+        C = contrastive_chunk()
+        ls = logit_scale.detach().reshape(1)
+        lab0 = rank * B
+        if Bg > C:
+            lse = torch.empty(2, B, dtype=torch.float32, device=dev)
+            ce = torch.empty(2, B, dtype=torch.float32, device=dev)
+            _ce_streamed_fwd(s, th, ig, ls, lab0, C, lse[0], ce[0])
+            _ce_streamed_fwd(s, ih, tg, ls, lab0, C, lse[1], ce[1])
+            loss = torch.empty((), dtype=torch.float32, device=dev)
+            call("clipmi_sum2", s, P_(ce[0]), P_(ce[1]), B, 1.0 / (2 * Bg), P_(loss), 0)
+            loss_out = loss
+            if world > 1 and global_loss:
+                loss_out = loss.clone()
+                dist.all_reduce(loss_out, group=group)
+            ctx.save_for_backward(th, ih, tn, inn, tg, ig, lse, ls)
+            ctx.group, ctx.world, ctx.B, ctx.Bg, ctx.lab0, ctx.chunk = group, world, B, Bg, lab0, C
+            ctx.ls_param, ctx.arena = logit_scale, arena
+            return loss_out, th, ih, None, None
+        ctx.chunk = None
         lt = torch.empty(B, Bg, dtype=torch.float32, device=dev)
         li = torch.empty(B, Bg, dtype=torch.float32, device=dev)
         _gemm_f32(B, Bg, E, th, E, True, ig, E, True, lt, Bg)   # cos(t_local, i_all)
         _gemm_f32(B, Bg, E, ih, E, True, tg, E, True, li, Bg)   # cos(i_local, t_all)
         lse = torch.empty(2, B, dtype=torch.float32, device=dev)
         ce = torch.empty(2, B, dtype=torch.float32, device=dev)
-        ls = logit_scale.detach().reshape(1)
-        lab0 = rank * B
         call("clipmi_contrastive_ce_fwd", s, P_(lt), P_(lt), P_(ls), B, Bg, lab0, P_(lse[0]), P_(ce[0]))
         call("clipmi_contrastive_ce_fwd", s, P_(li), P_(li), P_(ls), B, Bg, lab0, P_(lse[1]), P_(ce[1]))
         loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -746,6 +811,8 @@ class ContrastiveFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss, gth, gih, glt, gli):
+        if ctx.chunk is not None:
+            return ContrastiveFn._backward_streamed(ctx, gloss, gth, gih)
         th, ih, tn, inn, tg, ig, lt, li, lse, ls = ctx.saved_tensors
         B, Bg, E, world = ctx.B, ctx.Bg, th.shape[1], ctx.world
         dev = th.device
@@ -768,6 +835,34 @@ class ContrastiveFn(torch.autograd.Function):
         dih = _reduce_scatter(dIg, ctx.group, world)
         _gemm_f32(B, E, Bg, dSt, Bg, True, ig, E, False, dth, E, flags=_lib.EPI_BETA)
         _gemm_f32(B, E, Bg, dSi, Bg, True, tg, E, False, dih, E, flags=_lib.EPI_BETA)
+        return ContrastiveFn._finish_backward(ctx, s, dth, dih, gth, gih, dls, th, ih, tn, inn)
+
+    @staticmethod
+    def _backward_streamed(ctx, gloss, gth, gih):
+        th, ih, tn, inn, tg, ig, lse, ls = ctx.saved_tensors
+        B, Bg, E, world, C = ctx.B, ctx.Bg, th.shape[1], ctx.world, ctx.chunk
+        dev = th.device
+        s = K.stream()
+        gl = gloss.to(torch.float32).contiguous().reshape(1) if gloss is not None else None
+        dls = torch.empty(2, B, dtype=torch.float32, device=dev)
+        norm = 1.0 / (2 * Bg)
+        # logits_t = s t^_local i^_all^T feeds dt^ (rows) and di^_all (columns); logits_i the converse
+        dTg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
+        dIg = torch.empty(Bg, E, dtype=torch.float32, device=dev)
+        dth_row = torch.empty(B, E, dtype=torch.float32, device=dev)
+        dih_row = torch.empty(B, E, dtype=torch.float32, device=dev)
+        _ce_streamed_bwd(s, th, ig, ls, gl, lse[0], ctx.lab0, norm, C, dls[0], dIg, dth_row)
+        _ce_streamed_bwd(s, ih, tg, ls, gl, lse[1], ctx.lab0, norm, C, dls[1], dTg, dih_row)
+        dth = _reduce_scatter(dTg, ctx.group, world)
+        dih = _reduce_scatter(dIg, ctx.group, world)
+        dth += dth_row
+        dih += dih_row
+        return ContrastiveFn._finish_backward(ctx, s, dth, dih, gth, gih, dls, th, ih, tn, inn)
+
+    @staticmethod
+    def _finish_backward(ctx, s, dth, dih, gth, gih, dls, th, ih, tn, inn):
+        B, E = th.shape
+        dev = th.device
         if gth is not None:
             dth += gth
         if gih is not None:

@@ -88,6 +88,73 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* L, const float
   if (lane == 0) dls_row[row] = acc;
 }
 
+// Column-streamed form (config 5: Bg = 32768 at B = 4096/GPU): the [B, Bg] blocks are never
+// materialised; the caller walks column chunks [col0, col0 + C) of the cosine block.  Forward:
+// each chunk's row max / sum of exponentials merge into a running (max, sum) pair per row
+// (online log-sum-exp), and the label logit is kept when the label column falls in the chunk.
+// Backward: the same chunk is recomputed and turned into its dS slice.  Logits are formed as in
+// ce_fwd_kernel (v = S * exp(ls)), so a single chunk reproduces the unchunked kernels exactly.
+__global__ __launch_bounds__(256) void ce_fwd_chunk_kernel(const float* S, const float* logit_scale, int B, int C,
+                                                           int col0, int label0, float* run, float* lab) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float sc = __expf(*logit_scale);
+  const float* s = S + (int64_t)row * C;
+  float mx = -__builtin_huge_valf();
+  for (int j = lane; j < C; j += 64) mx = fmaxf(mx, s[j] * sc);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < C; j += 64) sum += __expf(s[j] * sc - mx);
+  sum = wave_sum(sum);
+  if (lane == 0) {
+    float* r = run + 2 * (int64_t)row;
+    if (col0 == 0) {
+      r[0] = mx;
+      r[1] = sum;
+    } else {
+      const float m = fmaxf(r[0], mx);
+      r[1] = r[1] * __expf(r[0] - m) + sum * __expf(mx - m);
+      r[0] = m;
+    }
+    const int lc = label0 + row - col0;
+    if (lc >= 0 && lc < C) lab[row] = s[lc] * sc;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_finish_kernel(const float* run, const float* lab, int B, float* lse_out,
+                                                        float* ce_out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  const float lse = run[2 * row] + __logf(run[2 * row + 1]);
+  lse_out[row] = lse;
+  ce_out[row] = lse - lab[row];
+}
+
+// one chunk of ce_bwd_kernel from the cosines: dS[:, 0:C) of columns col0.., dls_row (+)= its share
+__global__ __launch_bounds__(256) void ce_bwd_chunk_kernel(const float* S, const float* lse, const float* logit_scale,
+                                                           const float* gout, int B, int C, int col0, int label0,
+                                                           float norm, float* dS, float* dls_row, int beta) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float sc = __expf(*logit_scale);
+  const float g = (gout ? *gout : 1.f) * norm;
+  const float* s = S + (int64_t)row * C;
+  float* d = dS + (int64_t)row * C;
+  const float ls = lse[row];
+  const int lc = label0 + row - col0;
+  float acc = 0.f;
+  for (int j = lane; j < C; j += 64) {
+    const float l = s[j] * sc;
+    const float dl = g * (__expf(l - ls) - (j == lc ? 1.f : 0.f));
+    acc += dl * l;
+    d[j] = dl * sc;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) dls_row[row] = beta ? dls_row[row] + acc : acc;
+}
+
 // out[0] = scale * sum(a[0:n]) + scale * sum(b[0:n]) ; (beta) accumulate
 __global__ __launch_bounds__(1024) void sum2_kernel(const float* a, const float* b, int n, float scale, float* out,
                                                     int beta) {
@@ -134,6 +201,34 @@ extern "C" int clipmi_contrastive_ce_bwd(void* stream, const float* logits, cons
   CLIPMI_REQUIRE(label0 >= 0 && label0 + B <= Bg, "label offset out of range");
   hipLaunchKernelGGL(ce_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, lse, logit_scale,
                      grad_out, B, Bg, label0, norm, dS, dls_row);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_contrastive_ce_fwd_chunk(void* stream, const float* S, const float* logit_scale, int B, int C,
+                                               int col0, int Bg, int label0, float* run, float* lab) {
+  CLIPMI_REQUIRE(label0 >= 0 && label0 + B <= Bg, "label offset out of range");
+  CLIPMI_REQUIRE(C > 0 && col0 >= 0 && col0 + C <= Bg, "chunk out of range");
+  hipLaunchKernelGGL(ce_fwd_chunk_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, logit_scale, B, C,
+                     col0, label0, run, lab);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_contrastive_ce_finish(void* stream, const float* run, const float* lab, int B, float* lse,
+                                            float* ce) {
+  hipLaunchKernelGGL(ce_finish_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, run, lab, B, lse, ce);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_contrastive_ce_bwd_chunk(void* stream, const float* S, const float* lse, const float* logit_scale,
+                                               const float* grad_out, int B, int C, int col0, int Bg, int label0,
+                                               float norm, float* dS, float* dls_row, int beta) {
+  CLIPMI_REQUIRE(label0 >= 0 && label0 + B <= Bg, "label offset out of range");
+  CLIPMI_REQUIRE(C > 0 && col0 >= 0 && col0 + C <= Bg, "chunk out of range");
+  hipLaunchKernelGGL(ce_bwd_chunk_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, lse, logit_scale,
+                     grad_out, B, C, col0, label0, norm, dS, dls_row, beta);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
