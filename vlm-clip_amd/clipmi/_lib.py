@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libclipmi.so")
+# CLIPMI_LIB: an alternative build of the same library (schedule A/B experiments only)
+LIB_PATH = os.environ.get("CLIPMI_LIB") or os.path.join(_HERE, "libclipmi.so")
 
 F32, BF16, FP8 = 0, 1, 2
 EPI_BIAS, EPI_QGELU, EPI_GELU, EPI_RESID = 1, 2, 4, 8
