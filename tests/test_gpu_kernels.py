@@ -96,7 +96,7 @@ def attn_ref(qkv, B, N, H, mask, causal):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 50, 12, False), (2, 197, 12, False),
-                                           (3, 77, 8, True), (2, 256, 2, False),
+                                           (3, 77, 8, True), (2, 256, 2, False), (3, 150, 2, True),
                                            # ViT-L/14 at 224 (N = 257) and the N <= 288 limit
                                            (2, 257, 16, False), (3, 288, 2, False), (40, 257, 16, False),
                                            # more (batch, head) items than the persistent grid
@@ -169,6 +169,38 @@ def test_text_embedding_fwd_bwd(dtype):
     T.call("clipmi_text_embed", s, DT[dtype], ids_bad.data_ptr(), tok.data_ptr(), pos.data_ptr(), x0.data_ptr(),
            B * S, S, D, V, bad.data_ptr())
     assert bad.item() == 1
+
+
+@pytest.mark.parametrize("B,N,H,causal", [(4, 197, 12, False), (3, 150, 2, True), (2, 224, 3, False)])
+def test_attention_wave_count_invariant(B, N, H, causal, monkeypatch):
+    """The 16-wave whole-K/V kernels (one query / key block per wave) compute every block with the
+    same instruction sequence as the 8-wave ones (two blocks per wave): identical outputs."""
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 21, torch.bfloat16)
+    do = rnd((B * N, D), 22, torch.bfloat16)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(23)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    mp = mask.data_ptr() if mask is not None else None
+    s = kern.stream()
+    monkeypatch.setenv("CLIPMI_ATTN_FA", "0")
+    outs = []
+    for nw in ("8", "16"):
+        monkeypatch.setenv("CLIPMI_ATTN_FWD_NW", nw)
+        monkeypatch.setenv("CLIPMI_ATTN_BWD_NW", nw)
+        o = torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda")
+        lse = torch.empty(B * H * N, device="cuda")
+        dqkv = torch.empty_like(qkv)
+        T.call("clipmi_attention_fwd", s, DT[torch.bfloat16], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), mp,
+               int(causal), B, H, N, D)
+        T.call("clipmi_attention_bwd", s, DT[torch.bfloat16], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(),
+               do.data_ptr(), dqkv.data_ptr(), mp, int(causal), B, H, N, D)
+        torch.cuda.synchronize()
+        outs.append((o, lse, dqkv))
+    for a, b, nm in zip(outs[0], outs[1], ("O", "lse", "dqkv")):
+        assert torch.equal(a, b), nm
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

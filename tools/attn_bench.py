@@ -9,6 +9,7 @@ from clipmi import kernels as K, towers as T
 SHAPES = [("vision_b16", 1024, 197, 12, False), ("text", 1024, 77, 8, True), ("vision_l14", 512, 257, 16, False),
           ("vision_l14_336", 256, 577, 16, False)]
 only = sys.argv[1:] or None
+NWS = os.environ.get("ATTN_NWS", "16").split(",")  # whole-K/V kernels: waves per workgroup (A/B in one process)
 
 
 def timeit(f, n=10):
@@ -43,13 +44,17 @@ for name, B, N, H, causal in SHAPES:
                          B, H, N, D)
     bwd = lambda: T.call("clipmi_attention_bwd", s, 1, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
                          dqkv.data_ptr(), mp, int(causal), B, H, N, D)
-    for kern in ("pf", "fa"):
-        if kern == "pf" and N > 288:
-            continue
-        os.environ["CLIPMI_ATTN_FA"] = "1" if kern == "fa" else "0"
-        ms = timeit(fwd)
-        fl = 4.0 * B * H * N * npad * 64
-        print(f"{name:16s} fwd {kern}: {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
-    ms = timeit(bwd)
-    fl = 10.0 * B * H * N * npad * 64
-    print(f"{name:16s} bwd   : {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
+    for rep in range(2):
+        for nw in NWS:
+            os.environ["CLIPMI_ATTN_FWD_NW"] = os.environ["CLIPMI_ATTN_BWD_NW"] = nw
+            for kern in ("pf", "fa"):
+                if kern == "pf" and N > 288:
+                    continue
+                os.environ["CLIPMI_ATTN_FA"] = "1" if kern == "fa" else "0"
+                ms = timeit(fwd)
+                fl = 4.0 * B * H * N * npad * 64
+                print(f"{name:16s} nw{nw:>2s} fwd {kern}: {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
+            os.environ["CLIPMI_ATTN_FA"] = "0"
+            ms = timeit(bwd)
+            fl = 10.0 * B * H * N * npad * 64
+            print(f"{name:16s} nw{nw:>2s} bwd   : {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)

@@ -81,9 +81,9 @@ struct AttnP {
 // Q fragments for item i + 1 are loaded, while item i is computed.  DMAs are issued before
 // the Q loads so a wave's counted wait for its Q never waits on the ring.  Per wave: q-blocks
 // wave and wave + 8 of every item.
-template <int NKT, bool MASKED>
-__global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int nitems) {
-  constexpr int NPAD = NKT * 16, IMG = NPAD * 128, QPW = (NKT + 7) / 8;
+template <int NKT, bool MASKED, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 1) void attn_fwd_pf(AttnP p, int causal, int nitems) {
+  constexpr int NPAD = NKT * 16, IMG = NPAD * 128, QPW = (NKT + NW - 1) / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* keyok_base = (int*)(smem + 4 * IMG);  // [2][NPAD]
   const int t = threadIdx.x, lane = t & 63;
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
     const SRsrc rk = make_srsrc(base + D, rec), rv = make_srsrc(base + 2 * D, rec);
     char* kimg = smem + slot * 2 * IMG;
 #pragma unroll 1
-    for (int j = wave; j < NPAD / 8; j += 8) {
+    for (int j = wave; j < NPAD / 8; j += NW) {
       const int r = 8 * j + (lane >> 3);
       const int voff = r * (int)ld * 2 + (((lane & 7) ^ (r & 6)) << 4);
       dma16(rk, kimg + j * 1024, voff);
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
     }
     if (MASKED) {
       int* ko = keyok_base + slot * NPAD;
-      for (int k = t; k < NPAD; k += 512) ko[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
+      for (int k = t; k < NPAD; k += NW * 64) ko[k] = (k < N) && (!p.kmask || p.kmask[(int64_t)b * N + k] != 0);
     }
   };
   auto load_q = [&](int item, bf16x8 (&qf)[QPW][2]) {
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
     const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
 #pragma unroll
     for (int u = 0; u < QPW; ++u) {
-      const int qc = min((wave + 8 * u) * 16 + li, N - 1);
+      const int qc = min((wave + NW * u) * 16 + li, N - 1);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) qf[u][kk] = *(const bf16x8*)(base + (int64_t)qc * ld + kk * 32 + 8 * g);
     }
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
       bf16x8 pf[QPW][NKT / 2];
 #pragma unroll
       for (int u = 0; u < QPW; ++u) {
-        q[u] = (wave + 8 * u) * 16 + li;
+        q[u] = (wave + NW * u) * 16 + li;
         f32x4 sc[NKT];
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt) {
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pf(AttnP p, int causal, int n
       }
 #pragma unroll
       for (int u = 0; u < QPW; ++u) {
-        if (wave + 8 * u < nqb && q[u] < N) {
+        if (wave + NW * u < nqb && q[u] < N) {
           const float inv = l[u] > 0.f ? 1.f / l[u] : 0.f;
           bf16* orow = p.o + ((int64_t)b * N + q[u]) * D + h * 64;
 #pragma unroll
@@ -604,7 +604,7 @@ struct BwdCtx {
 
 // dK, dV of the wave's NB key blocks (kb = wave, wave + NW): K/V fragments in registers,
 // Q/dO images in LDS.
-template <bool CAUSAL, int NB>
+template <bool CAUSAL, int NB, bool LOWREG = false>
 __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[2][2], const bf16x8 (&vf)[2][2],
                                             int wave, int NW) {
   const int lane = c.lane, g = lane >> 4, li = lane & 15;
@@ -651,6 +651,7 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
           ds[u][tau][r] = pv * (dp[r] - d4[r]);
         }
       }
+      if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);  // one tau's operands live at a time
     }
     bf16x8 pf[NB], sf[NB];
 #pragma unroll
@@ -685,7 +686,7 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
 
 // dQ of the wave's NB query blocks (qb = wave, wave + NW): Q/dO fragments in registers, K/V
 // images in LDS; the blocks advance together over the keys, sharing every K/V read.
-template <bool CAUSAL, int NB>
+template <bool CAUSAL, int NB, bool LOWREG = false>
 __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[2][2], const bf16x8 (&of)[2][2],
                                             int wave, int NW) {
   const int lane = c.lane, g = lane >> 4, li = lane & 15;
@@ -731,6 +732,7 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
           ds[u][tau][r] = pv * (dp[r] - dl[u]);
         }
       }
+      if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
     }
     bf16x8 sf[NB];
 #pragma unroll
@@ -759,6 +761,9 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
 template <bool CAUSAL, int NW>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   constexpr int NT = NW * 64;
+  // key / query blocks per wave: two with 8 waves (N <= 256), one with 16 (N <= 256: 4 waves per
+  // SIMD, 128 registers each, so one wave's MFMA -> exp -> MFMA chain hides behind three others)
+  constexpr int NBM = NW >= 16 ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -807,7 +812,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   auto load_kvfrag = [&](int item, bf16x8 (&kf)[2][2], bf16x8 (&vf)[2][2]) {
     const bf16* base = qkv_of(item);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NBM; ++u) {
       const int key = min((wave + NW * u) * 16 + li, N - 1);  // rows past N are masked by keyok
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -871,7 +876,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     // ---- phase A: dK, dV (Q image, dO image); a wave with two key blocks advances them
     // together so each Q/dO fragment read from LDS feeds both
     // (causal: blocks far apart need different query ranges, so they run one at a time)
-    if (!CAUSAL && wave + NW < nkb) {
+    if constexpr (NBM == 1) {
+      if (wave < nkb) bwd_phase_a<CAUSAL, 1, true>(c, kf, vf, wave, NW);
+    } else if (!CAUSAL && wave + NW < nkb) {
       bwd_phase_a<CAUSAL, 2>(c, kf, vf, wave, NW);
     } else {
       if (wave < nkb) bwd_phase_a<CAUSAL, 1>(c, kf, vf, wave, NW);
@@ -895,7 +902,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     const int nqb = (N + 15) >> 4;
     bf16x8 qf[2][2], of[2][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NBM; ++u) {
       const int q = min((wave + NW * u) * 16, NPAD - 16) + li;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -905,7 +912,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     }
     raw_barrier_lds();  // every wave holds its Q/dO fragments: the images may be overwritten
     if (more) issue_qdo(nxt);
-    if (!CAUSAL && wave + NW < nqb) {
+    if constexpr (NBM == 1) {
+      if (wave < nqb) bwd_phase_b<CAUSAL, 1, true>(c, qf, of, wave, NW);
+    } else if (!CAUSAL && wave + NW < nqb) {
       bwd_phase_b<CAUSAL, 2>(c, qf, of, wave, NW);
     } else {
       if (wave < nqb) bwd_phase_b<CAUSAL, 1>(c, qf, of, wave, NW);
@@ -1312,10 +1321,21 @@ template <int NKT, bool M>
 void launch_fwd_pf(const AttnP& p, int causal, hipStream_t s) {
   constexpr int NPAD = NKT * 16;
   constexpr size_t lds = 4 * (size_t)NPAD * 128 + 2 * NPAD * sizeof(int);
-  (void)lds_optin((const void*)attn_fwd_pf<NKT, M>, (int)lds);
   const int nitems = p.B * p.H;
   const int per_cu = (int)std::min<size_t>(2, (160 * 1024) / lds);
   const int grid = std::min(nitems, 256 * per_cu);
+  // 16 waves (one query block each, 4 per SIMD) where one workgroup fills the CU and the blocks
+  // need more than 8 waves; CLIPMI_ATTN_FWD_NW=8 selects the 8-wave form (A/B hook, read per call)
+  const char* e = getenv("CLIPMI_ATTN_FWD_NW");
+  const bool w16 = (e ? atoi(e) : 16) == 16 && NKT > 8 && NKT <= 16 && per_cu == 1;
+  if constexpr (NKT > 8 && NKT <= 16) {  // NKT = 18 (L/14) spills at 128 registers
+    if (w16) {
+      (void)lds_optin((const void*)attn_fwd_pf<NKT, M, 16>, (int)lds);
+      hipLaunchKernelGGL((attn_fwd_pf<NKT, M, 16>), dim3(grid), dim3(1024), lds, s, p, causal, nitems);
+      return;
+    }
+  }
+  (void)lds_optin((const void*)attn_fwd_pf<NKT, M>, (int)lds);
   hipLaunchKernelGGL((attn_fwd_pf<NKT, M>), dim3(grid), dim3(512), lds, s, p, causal, nitems);
 }
 
@@ -1350,8 +1370,16 @@ void launch_bwd_pf(const AttnP& p, hipStream_t s) {
 // 4 waves per workgroup for N <= 128 (text: 5 blocks of 16 rows), else 8; each wave owns at
 // most 2 key blocks and 2 query blocks.
 int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
+  // CLIPMI_ATTN_BWD_NW=16 (A/B hook, read per call): one block per wave, 4 waves per SIMD.  Measured
+  // 3-5 % slower than 8 waves at N = 197 (profiles/r02_attn_waves_ab.log): this backward is bound by
+  // its LDS fragment traffic (each wave re-reads the Q/dO and K/V fragments of every step), which
+  // two blocks per wave share and one block per wave does not
+  const char* e = getenv("CLIPMI_ATTN_BWD_NW");
+  const int nw = e ? atoi(e) : 8;
   if (p.N <= 128) {
     if (causal) launch_bwd_pf<true, 4>(p, s); else launch_bwd_pf<false, 4>(p, s);
+  } else if (nw == 16 && p.N <= 256) {
+    if (causal) launch_bwd_pf<true, 16>(p, s); else launch_bwd_pf<false, 16>(p, s);
   } else {
     if (causal) launch_bwd_pf<true, 8>(p, s); else launch_bwd_pf<false, 8>(p, s);
   }
