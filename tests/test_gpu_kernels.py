@@ -330,6 +330,25 @@ def test_adamw_and_clip_match_torch():
     assert rel(shadow, p_ref.detach()) < 1e-2
 
 
+def test_adamw_vector_path_is_bitwise_scalar_path():
+    """16-B-aligned arenas take the 4-per-lane AdamW kernel, a 4-B offset the scalar one: same bits."""
+    n = 50_001
+    outs = []
+    for off in (0, 1):  # element offset 0: aligned (vector body + tail); 1: misaligned (scalar)
+        bufs = [torch.zeros(n + 4, device="cuda") for _ in range(4)]
+        for i, b in enumerate(bufs):
+            b[off:off + n] = rnd((n,), 40 + i)
+        p, g, m, v = (b[off:off + n] for b in bufs)
+        v.abs_()
+        sh = torch.empty(n + 4, dtype=torch.bfloat16, device="cuda")[off:off + n]
+        T.call("clipmi_adamw", kern.stream(), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+               sh.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3, None)
+        torch.cuda.synchronize()
+        outs.append([p.clone(), m.clone(), v.clone(), sh.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tag", ["sq", "crop"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("P", [16, 14])

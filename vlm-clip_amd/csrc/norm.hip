@@ -157,8 +157,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
   for (int k = 0; k < NP; ++k) vload<T, PS>(w + (k * 64 + lane) * PS, wv[k]);
   for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
-    float g[NP][PS], xh[NP][PS];
+    float g[NP][PS], xh[NP][PS], rr[NP][PS];
     float s1 = 0.f, s2 = 0.f;
+    if (dres) {  // the residual gradient is independent of the reductions: in flight beside dy and x
+#pragma unroll
+      for (int k = 0; k < NP; ++k) vload<T, PS>(dres + (int64_t)row * ldres + (k * 64 + lane) * PS, rr[k]);
+    }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int c = (k * 64 + lane) * PS;
@@ -184,10 +188,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
 #pragma unroll
       for (int j = 0; j < PS; ++j) o[j] = rs * (g[k][j] - s1 - xh[k][j] * s2);
       if (dres) {
-        float r[PS];
-        vload<T, PS>(dres + (int64_t)row * ldres + c, r);
 #pragma unroll
-        for (int j = 0; j < PS; ++j) o[j] += r[j];
+        for (int j = 0; j < PS; ++j) o[j] += rr[k][j];
       }
       vstore<T, PS>(dx + (int64_t)row * lddx + c, o);
     }

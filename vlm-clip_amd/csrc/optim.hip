@@ -53,18 +53,47 @@ __global__ __launch_bounds__(1024) void norm_finish_kernel(const float* part, in
 // torch.optim.AdamW (foreach=False semantics):
 //   p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
 //   p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+__device__ __forceinline__ float adamw_elem(float gi, float& pi, float& mi, float& vi, float cf, float step, float decay,
+                                            float b1, float b2, float eps, float bc2s) {
+  gi *= cf;
+  pi *= decay;
+  mi = mi + (1.f - b1) * (gi - mi);  // exp_avg.lerp_(grad, 1 - beta1)
+  vi = b2 * vi + (1.f - b2) * gi * gi;
+  pi -= step * mi / (sqrtf(vi) / bc2s + eps);
+  return pi;
+}
+
+// 4 parameters per lane (16-B loads/stores, 8-B shadow stores; cdna_hip_programming.md G13),
+// scalar tail; the per-element arithmetic is adamw_elem's either way
+template <bool VEC>
 __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* shadow,
                                                     int64_t n, float lr, float b1, float b2, float eps, float wd,
                                                     float bc1, float bc2s, const float* clip) {
   const float cf = clip ? clip[1] : 1.f;
   const float step = lr / bc1;  // step_size = lr / bias_correction1
   const float decay = 1.f - lr * wd;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = g[i] * cf;
-    float pi = p[i] * decay;
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    pi -= step * mi / (sqrtf(vi) / bc2s + eps);
+  const int64_t n4 = VEC ? n / 4 : 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    const f32x4 gv = ((const f32x4*)g)[i];
+    f32x4 pv = ((const f32x4*)p)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], me = mv[e], ve = vv[e];
+      adamw_elem(gv[e], pe, me, ve, cf, step, decay, b1, b2, eps, bc2s);
+      pv[e] = pe; mv[e] = me; vv[e] = ve;
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    if (shadow) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      ((bf16x4*)shadow)[i] = bf16x4{(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+    }
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(g[i], pi, mi, vi, cf, step, decay, b1, b2, eps, bc2s);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -127,9 +156,16 @@ extern "C" int clipmi_adamw(void* stream, float* p, const float* g, float* m, fl
   // bias corrections in double, as torch computes them on the host
   const double bc1 = 1.0 - pow(beta1, (double)step);
   const double bc2s = sqrt(1.0 - pow(beta2, (double)step));
-  hipLaunchKernelGGL(adamw_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)shadow_bf16, n,
-                     (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1, (float)bc2s,
-                     clip);
+  const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                   ((uintptr_t)shadow_bf16 & 7) == 0;
+  if (vec)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(4096), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)shadow_bf16,
+                       n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
+                       (float)bc2s, clip);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(4096), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)shadow_bf16,
+                       n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
+                       (float)bc2s, clip);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
