@@ -1037,15 +1037,20 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
     const char* Vimg = Kimg + FA_TILE / 2;
     const int k0 = kt * FA_KT;
     const int nsteps = min(2, (N - k0 + 31) >> 5);  // 32-key steps holding valid keys
+    // Unmasked (vision): the block loop is straight-line code -- every block computed (rows past N
+    // read zero-filled Q), every 32-key step computed (keys past N get P = 0), the offset moved
+    // per lane by select -- so the compiler interleaves one block's MFMAs with another's softmax.
 #pragma unroll
     for (int u = 0; u < QPW; ++u) {
-      if (!qv[u]) continue;
-      if (causal && k0 > q0 + (wave + FA_W * u) * 16 + 15) continue;  // every key follows every query
+      if constexpr (MASKED) {
+        if (!qv[u]) continue;
+        if (causal && k0 > q0 + (wave + FA_W * u) * 16 + 15) continue;  // every key follows every query
+      }
       f32x4 sc[4];
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         sc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (st < 2 * nsteps) {
+        if (!MASKED || st < 2 * nsteps) {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
             sc[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kimg, st * 16 + li, kk * 4 + g), qf[u][kk],
@@ -1068,7 +1073,17 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mt2 = mt * c2;
       // deferred maximum: move the offset only when this tile's max exceeds it by > FA_THR
-      if (__builtin_amdgcn_read_exec() && __any(mt2 > m[u] + FA_THR)) {
+      if constexpr (!MASKED) {  // every tile holds a valid key: mt2 finite; the row's 4 lanes agree
+        const float mn = mt2 > m[u] + FA_THR ? fmaxf(m[u], mt2) : m[u];
+        const float f = __builtin_amdgcn_exp2f(m[u] - mn);  // 1 unmoved, 0 on the first tile
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+        m[u] = mn;
+      } else if (__builtin_amdgcn_read_exec() && __any(mt2 > m[u] + FA_THR)) {
         const float mn = fmaxf(m[u], mt2);
         const float f = m[u] == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m[u] - mn);
 #pragma unroll
@@ -1089,7 +1104,7 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
       pf[1] = pack8(sc[2], sc[3]);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if (ks < nsteps) {
+        if (!MASKED || ks < nsteps) {
           accl[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[ks], accl[u], 0, 0, 0);
 #pragma unroll
           for (int v = 0; v < 4; ++v)

@@ -74,21 +74,35 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
   const float decay = 1.f - lr * wd;
   const int64_t n4 = VEC ? n / 4 : 0;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-    const f32x4 gv = ((const f32x4*)g)[i];
-    f32x4 pv = ((const f32x4*)p)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+  // two 4-parameter groups per lane and iteration: all eight 16-B loads in flight before the math
+  constexpr int U = 2;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += U * stride) {
+    f32x4 gv[U], pv[U], mv[U], vv[U];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pv[e], me = mv[e], ve = vv[e];
-      adamw_elem(gv[e], pe, me, ve, cf, step, decay, b1, b2, eps, bc2s);
-      pv[e] = pe; mv[e] = me; vv[e] = ve;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = min(i0 + u * stride, n4 - 1);  // a clamped duplicate rewrites the same values
+      gv[u] = ((const f32x4*)g)[i];
+      pv[u] = ((const f32x4*)p)[i];
+      mv[u] = ((const f32x4*)m)[i];
+      vv[u] = ((const f32x4*)v)[i];
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)m)[i] = mv;
-    ((f32x4*)v)[i] = vv;
-    if (shadow) {
-      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-      ((bf16x4*)shadow)[i] = bf16x4{(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) break;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = pv[u][e], me = mv[u][e], ve = vv[u][e];
+        adamw_elem(gv[u][e], pe, me, ve, cf, step, decay, b1, b2, eps, bc2s);
+        pv[u][e] = pe; mv[u][e] = me; vv[u][e] = ve;
+      }
+      ((f32x4*)p)[i] = pv[u];
+      ((f32x4*)m)[i] = mv[u];
+      ((f32x4*)v)[i] = vv[u];
+      if (shadow) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        ((bf16x4*)shadow)[i] = bf16x4{(bf16)pv[u][0], (bf16)pv[u][1], (bf16)pv[u][2], (bf16)pv[u][3]};
+      }
     }
   }
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
