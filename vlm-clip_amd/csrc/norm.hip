@@ -155,43 +155,59 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
   float wv[NP][PS];
 #pragma unroll
   for (int k = 0; k < NP; ++k) vload<T, PS>(w + (k * 64 + lane) * PS, wv[k]);
-  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float g[NP][PS], xh[NP][PS], rr[NP][PS];
-    float s1 = 0.f, s2 = 0.f;
-    if (dres) {  // the residual gradient is independent of the reductions: in flight beside dy and x
+  // rows per wave and iteration, every load of them (dres, dy, x) issued before the first
+  // reduction (as ln_fwd_kernel).  Two rows for D <= 512 (text: 67 -> 65 us at R = 78,848); one for
+  // wider rows, where two rows' registers (164 VGPRs at D = 768) cost a wave per SIMD and measured
+  // 3-4 % slower (tools/ln_bench.py, profiles/r02_ln_bwd_ab.log)
+  constexpr int RPW = NP * PS <= 8 ? 2 : 1;
+  for (int row0 = (blockIdx.x * 4 + wave) * RPW; row0 < R; row0 += gridDim.x * 4 * RPW) {
+    float g[RPW][NP][PS], xh[RPW][NP][PS], rr[RPW][NP][PS], d[RPW][NP][PS];
+    float mu[RPW], rs[RPW];
 #pragma unroll
-      for (int k = 0; k < NP; ++k) vload<T, PS>(dres + (int64_t)row * ldres + (k * 64 + lane) * PS, rr[k]);
-    }
+    for (int q = 0; q < RPW; ++q) {
+      const int row = min(row0 + q, R - 1);  // a clamped duplicate row is computed, not stored
+      mu[q] = mean[row];
+      rs[q] = rstd[row];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int c = (k * 64 + lane) * PS;
-      float d[PS], xv[PS];
-      vload<T, PS>(dy + (int64_t)row * lddy + c, d);
-      vload<T, PS>(x + (int64_t)row * ldx + c, xv);
-#pragma unroll
-      for (int j = 0; j < PS; ++j) {
-        xh[k][j] = (xv[j] - mu) * rs;
-        g[k][j] = d[j] * wv[k][j];
-        s1 += g[k][j];
-        s2 += g[k][j] * xh[k][j];
-        pg[k][j] += d[j] * xh[k][j];
-        pb[k][j] += d[j];
+      for (int k = 0; k < NP; ++k) {
+        const int c = (k * 64 + lane) * PS;
+        if (dres) vload<T, PS>(dres + (int64_t)row * ldres + c, rr[q][k]);
+        vload<T, PS>(dy + (int64_t)row * lddy + c, d[q][k]);
+        vload<T, PS>(x + (int64_t)row * ldx + c, xh[q][k]);
       }
     }
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int c = (k * 64 + lane) * PS;
-      float o[PS];
+    for (int q = 0; q < RPW; ++q) {
+      const bool live = row0 + q < R;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < PS; ++j) o[j] = rs * (g[k][j] - s1 - xh[k][j] * s2);
-      if (dres) {
+      for (int k = 0; k < NP; ++k)
 #pragma unroll
-        for (int j = 0; j < PS; ++j) o[j] += rr[k][j];
+        for (int j = 0; j < PS; ++j) {
+          xh[q][k][j] = (xh[q][k][j] - mu[q]) * rs[q];
+          g[q][k][j] = d[q][k][j] * wv[k][j];
+          s1 += g[q][k][j];
+          s2 += g[q][k][j] * xh[q][k][j];
+          if (live) {
+            pg[k][j] += d[q][k][j] * xh[q][k][j];
+            pb[k][j] += d[q][k][j];
+          }
+        }
+      s1 = wave_sum(s1) / D;
+      s2 = wave_sum(s2) / D;
+      if (!live) continue;
+      const int row = row0 + q;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int c = (k * 64 + lane) * PS;
+        float o[PS];
+#pragma unroll
+        for (int j = 0; j < PS; ++j) {
+          o[j] = rs[q] * (g[q][k][j] - s1 - xh[q][k][j] * s2);
+          if (dres) o[j] += rr[q][k][j];
+        }
+        vstore<T, PS>(dx + (int64_t)row * lddx + c, o);
       }
-      vstore<T, PS>(dx + (int64_t)row * lddx + c, o);
     }
   }
   if (!ws) return;
@@ -490,10 +506,23 @@ void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t*
                        (const T*)nullptr, (const T*)nullptr, 1, q8, s8);
   }
 }
+// grid (in: the partial-sum rows the workspace holds; out: the blocks launched = partial rows
+// written): at most the blocks the CUs hold at once, so no block starts a second round late
+// (the D = 768 form keeps two rows' loads in registers: 164 VGPRs, 3 waves per SIMD)
 template <typename T, int PS, int NP>
-void ln_bwd_launch(hipStream_t s, int grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+void ln_bwd_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                    int64_t ldres, float* ws, int R, int D) {
+  static int resident = [] {
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<T, PS, NP>, 256, 0) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    return per_cu * cus;
+  }();
+  if (grid > resident) grid = resident;
   hipLaunchKernelGGL((ln_bwd_kernel<T, PS, NP>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const T*)x, ldx,
                      mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
 }
