@@ -1675,12 +1675,24 @@ __global__ __launch_bounds__(256) void bias_partials_reduce_kernel(const float* 
   bias_grad[m] += acc;
 }
 
+// Blocks nmain.. (when bws is set) sum the fused bias-gradient partials in split order, as
+// bias_partials_reduce_kernel does, so a weight gradient with its bias costs one reduce launch.
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* ws, float* C, int64_t ldc, int M, int N,
-                                                             int splits, float alpha, int beta) {
+                                                             int splits, float alpha, int beta, int nmain,
+                                                             const float* bws, float* bias_grad) {
+  if ((int)blockIdx.x >= nmain) {
+    const int m = ((int)blockIdx.x - nmain) * 256 + threadIdx.x;
+    if (m < M) {
+      float acc = 0.f;
+      for (int z = 0; z < splits; ++z) acc += bws[(int64_t)z * M + m];
+      bias_grad[m] += acc;
+    }
+    return;
+  }
   const int64_t total = (int64_t)M * N;
   const int n4 = N >> 2;
   const int64_t total4 = (int64_t)M * n4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)nmain * blockDim.x) {
     const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
     const float* src = ws + (int64_t)m * N + n;
     float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2026,17 +2038,19 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     const int64_t total = (int64_t)d->M * d->N;
     const int beta = (d->flags & CLIPMI_EPI_BETA) ? 1 : 0;
     if (d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0 && ((uintptr_t)p.ws & 15) == 0) {
-      const unsigned nblk = (unsigned)std::min<int64_t>((total / 4 + 255) / 256, 65536);
-      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(nblk), dim3(256), 0, s,
-                         p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta);
+      const int nblk = (int)std::min<int64_t>((total / 4 + 255) / 256, 65536);
+      const int nbias = p.bws ? (d->M + 255) / 256 : 0;
+      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(nblk + nbias), dim3(256), 0, s,
+                         p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta, nblk, (const float*)p.bws,
+                         d->bias_grad);
     } else {
       const unsigned nblk = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
                          p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta);
+      if (p.bws)
+        hipLaunchKernelGGL(bias_partials_reduce_kernel, dim3((d->M + 255) / 256), dim3(256), 0, s, p.bws,
+                           d->bias_grad, d->M, splits);
     }
-    if (p.bws)
-      hipLaunchKernelGGL(bias_partials_reduce_kernel, dim3((d->M + 255) / 256), dim3(256), 0, s, p.bws, d->bias_grad,
-                         d->M, splits);
     CLIPMI_CHECK_LAUNCH();
   }
   return CLIPMI_OK;
