@@ -6,8 +6,10 @@
 // All trainable parameters live in one fp32 arena (p, grad, exp_avg, exp_avg_sq), so
 // the step is 2 launches: a deterministic two-stage sum of squares, then one fused
 // elementwise AdamW pass that reads the clip coefficient from device memory and also
-// refreshes the bf16 shadow the MFMA kernels read.  HBM-bound: 28 B/param
-// (p, g, m, v read; p, m, v written) + 2 B/param shadow.
+// refreshes the bf16 shadow the MFMA kernels read.  28 B/param (p, g, m, v read; p, m, v
+// written) + 2 B/param shadow, at 5.4-5.5 TB/s over the B/16 arena (tools/optim_bench.py): near
+// the HBM rate, with the IEEE sqrt and two divisions per parameter (torch's arithmetic) making
+// it VALU-heavy enough that fp-contraction changes show (profiles/r02_adamw_ab.txt).
 #include "common.h"
 #include "internal.h"
 
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
     f32x4 gv[U], pv[U], mv[U], vv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t i = min(i0 + u * stride, n4 - 1);  // a clamped duplicate rewrites the same values
+      const int64_t i = min(i0 + u * stride, n4 - 1);  // past the end: a clamped load, never stored
       gv[u] = ((const f32x4*)g)[i];
       pv[u] = ((const f32x4*)p)[i];
       mv[u] = ((const f32x4*)m)[i];
