@@ -171,7 +171,8 @@ def test_text_embedding_fwd_bwd(dtype):
     assert bad.item() == 1
 
 
-@pytest.mark.parametrize("B,N,H,causal", [(4, 197, 12, False), (3, 150, 2, True), (2, 224, 3, False)])
+@pytest.mark.parametrize("B,N,H,causal", [(4, 197, 12, False), (3, 150, 2, True), (2, 224, 3, False),
+                                           (2, 129, 2, False), (2, 255, 2, False)])
 def test_attention_wave_count_invariant(B, N, H, causal, monkeypatch):
     """The 16-wave whole-K/V kernels (one query / key block per wave) compute every block with the
     same instruction sequence as the 8-wave ones (two blocks per wave): identical outputs."""
@@ -330,11 +331,12 @@ def test_adamw_and_clip_match_torch():
     assert rel(shadow, p_ref.detach()) < 1e-2
 
 
-def test_adamw_vector_path_matches_scalar_path():
+@pytest.mark.parametrize("n", [50_001, 9_000_011])  # the second spans both 4-parameter groups of a lane
+def test_adamw_vector_path_matches_scalar_path(n):
     """16-B-aligned arenas take the 4-per-lane AdamW kernel, a 4-B offset the scalar one: the same
     update to the last bit or two (the compiler may contract a mul+add into an fma differently in
-    the packed body; each path is itself deterministic)."""
-    n = 50_001
+    the packed body; each path is itself deterministic).  n = 9,000,011 > 2 x 4096 x 256 x 4 runs the
+    second parameter group of every lane and the clamped tail of the grid-stride loop."""
     outs = []
     for off in (0, 1):  # element offset 0: aligned (vector body + tail); 1: misaligned (scalar)
         bufs = [torch.zeros(n + 4, device="cuda") for _ in range(4)]
