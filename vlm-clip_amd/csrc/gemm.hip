@@ -1781,11 +1781,11 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
     case 4: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
     case 9: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
     case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); break;  // no epilogue (timing)
+#ifdef CLIPMI_GEMM_EXPERIMENTS  // schedule A/B variants (measured, not production); build with EXTRA=-DCLIPMI_GEMM_EXPERIMENTS
     case 13: launch_ppv<AK, BKM, OutT, EPI, BG, 16>(p, splits, s, bias_grad); break;  // DMAs between MFMAs
     case 14: launch_ppv<AK, BKM, OutT, EPI, BG, 20>(p, splits, s, bias_grad); break;  // + no setprio
     case 15: launch_ppv<AK, BKM, OutT, EPI, BG, 32>(p, splits, s, bias_grad); break;  // stores through LDS
     case 16: launch_ppv<AK, BKM, OutT, EPI, BG, 64>(p, splits, s, bias_grad); break;  // direct stores only
-#ifdef CLIPMI_GEMM_EXPERIMENTS
     case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
     case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
     case 7: launch_ppv<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
