@@ -300,7 +300,7 @@ def main():
                              fast_init=True, process_group=group)
     params = [p for n, p in model.named_parameters() if p.requires_grad]
     opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas(), process_group=group)
-    opt.overlap_with(model)  # world > 1: gradient buckets all-reduced under the backward
+    opt.overlap_with(model)  # world > 1: gradient buckets all-reduced under the backward (armed_backward)
     batch = synthetic_batch(cfg, args.batch, rank, dev)
     total = args.warmup + args.steps
 
@@ -308,7 +308,7 @@ def main():
         out = model(**batch)
         loss = out["loss"]
         opt.zero_grad()
-        loss.backward()
+        opt.armed_backward(loss)
         if world > 1:
             opt.grads_all_reduce(group)
         opt.clip_grad_norm(1.0)

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q, overlap=False, chunk=None):
+def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False):
     import sys
     if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
         os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
@@ -24,7 +24,7 @@ def _worker(rank, world, port, q, overlap=False, chunk=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    m = CLIPWithAdapters("tiny", use_text_adapter=True, use_vision_adapter=True, use_shared_adapters=False,
+    m = CLIPWithAdapters("tiny", use_text_adapter=True, use_vision_adapter=True, use_shared_adapters=shared,
                          freeze_clip=False, device="cuda:0", precision="fp32", pooling="eos",
                          process_group=dist.group.WORLD)
     B = 4
@@ -36,7 +36,7 @@ def _worker(rank, world, port, q, overlap=False, chunk=None):
         opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas())
     opt.zero_grad()
     out = m(**b)
-    out["loss"].backward()
+    opt.armed_backward(out["loss"])
     opt.grads_all_reduce(dist.group.WORLD)
     torch.cuda.synchronize()
     g = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters() if p.grad is not None}
@@ -45,21 +45,24 @@ def _worker(rank, world, port, q, overlap=False, chunk=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,chunk", [(False, None), (True, None), (False, 3)])
-def test_two_rank_data_parallel_matches_single_device(overlap, chunk):
+@pytest.mark.parametrize("overlap,chunk,shared", [(False, None, False), (True, None, False), (False, 3, False),
+                                                  (True, None, True)])
+def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared):
+    """shared=True: shared adapters on an unfrozen CLIP add a position-embedding gradient after the
+    vision tower's backward, so the overlapped reducer must leave that block to finish()."""
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500
-    port += 37 * int(overlap) + 71 * int(chunk is not None)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk)) for r in range(2)]
+    port += 37 * int(overlap) + 71 * int(chunk is not None) + 113 * int(shared)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk, shared)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(120)
-    m = CLIPWithAdapters("tiny", use_shared_adapters=False, freeze_clip=False, device="cuda:0", precision="fp32",
+    m = CLIPWithAdapters("tiny", use_shared_adapters=shared, freeze_clip=False, device="cuda:0", precision="fp32",
                          pooling="eos")
     b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, 8, seed=5).items()}
     out = m(**b)

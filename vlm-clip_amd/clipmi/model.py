@@ -36,6 +36,7 @@ class _Runtime:
         self.train_tower = False
         self.bad_flag = torch.zeros(1, dtype=torch.int32, device=self.arena.device)
         self.grad_hook = None  # data-parallel gradient-ready hook (CLIPWithAdapters.set_grad_hook)
+        self.shared_pos_grad = False  # a shared adapter adds into the vision position-embedding grad
         self.fp8 = False  # precision="fp8": the frozen towers' GEMMs in MXFP8 (BASELINE config 5)
 
 
@@ -231,6 +232,9 @@ class CLIPWithAdapters(nn.Module):
             from .shared_adapter import SharedAdapterFn
             # the Parameter itself, so an unfrozen CLIP gets this path's position-embedding gradient
             pos = self.clip.vision_model.embeddings.position_embedding.weight
+            # the shared adapters' position-embedding gradient lands after the vision tower's
+            # backward: the tower must then leave its embedding block to the reducer's finish()
+            self._rt.shared_pos_grad = torch.is_grad_enabled() and pos.requires_grad
             for sa in self.shared_adapters:
                 need = self._adapter_needs_grad(sa, h) or (torch.is_grad_enabled() and pos.requires_grad)
                 h = SharedAdapterFn.apply(h, _anchor(sa), sa, pos, need)

@@ -63,8 +63,18 @@ class SharedAdapterParams(ArenaModule):
         self.drop_offset = 0
 
     def dropout_mask(self, n, device):
+        """Counter-based keep mask for the next n elements.  Replay: a mask is a pure function of
+        (drop_seed, rank, drop_offset, n); the offset advances by n on every training-mode call,
+        so re-running the same calls from the same drop_offset reproduces the masks.  In a
+        data-parallel group the rank is mixed into the seed, so ranks draw different masks for
+        their different samples (as independent torch RNG streams would)."""
         keep = torch.empty(n, dtype=torch.uint8, device=device)
-        call("clipmi_dropout_mask", K.stream(), P_(keep), n, self.p, self.drop_seed, self.drop_offset)
+        seed = self.drop_seed
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            r = torch.distributed.get_rank()
+            if r:
+                seed = (seed ^ ((r * 0x9E3779B97F4A7C15) & (2 ** 64 - 1))) & (2 ** 63 - 1)
+        call("clipmi_dropout_mask", K.stream(), P_(keep), n, self.p, seed, self.drop_offset)
         self.drop_offset += n
         return keep
 

@@ -420,7 +420,10 @@ class VisionTowerFn(torch.autograd.Function):
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
              arena.ptr("vision_model.embeddings.position_embedding.weight", g), 1)
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, 1, D, arena.ptr("vision_model.embeddings.class_embedding", g), 1)
-        if hook is not None:  # class / patch / position embeddings + pre_layrnorm: one contiguous block
+        # class / patch / position embeddings + pre_layrnorm: one contiguous block.  Not final when
+        # a shared adapter still has to add its position-embedding gradient (its backward runs
+        # after this one): the reducer's finish() then takes the block
+        if hook is not None and not getattr(rt, "shared_pos_grad", False):
             lo = arena.offsets["vision_model.embeddings.class_embedding"][0]
             hi = arena.offsets["vision_model.encoder.layers.0.layer_norm1.weight"][0]
             hook(arena, lo, hi - lo)
@@ -702,12 +705,17 @@ def _reduce_scatter(x, group, world):
     return y[r * n:(r + 1) * n].contiguous()
 
 
-def contrastive_chunk():
+def contrastive_chunk(world=2):
     """Columns per chunk of the column-streamed contrastive (CLIPMI_CE_CHUNK, default 8192): a
-    global batch wider than this is never materialised as [B, Bg] blocks (BASELINE config 5:
-    Bg = 32768 at B = 4096 per GPU would be four 512 MiB fp32 blocks); at config 3 (Bg <= 8192)
-    the whole block is one chunk and the plain path runs."""
-    return max(1, int(os.environ.get("CLIPMI_CE_CHUNK", "8192")))
+    data-parallel global batch wider than this is never materialised as [B, Bg] blocks (BASELINE
+    config 5: Bg = 32768 at B = 4096 per GPU would be four 512 MiB fp32 blocks); at config 3
+    (Bg <= 8192) the whole block is one chunk and the plain path runs.  On one device the logits
+    are always materialised unless CLIPMI_CE_CHUNK is set explicitly: the reference's forward
+    returns logits_per_text / logits_per_image (model_m.py:165-176), and callers index them."""
+    env = os.environ.get("CLIPMI_CE_CHUNK")
+    if env is None and world == 1:
+        return 1 << 62
+    return max(1, int(env or "8192"))
 
 
 def _ce_streamed_fwd(s, x_local, y_all, ls, lab0, C, lse, ce):
@@ -767,7 +775,7 @@ class ContrastiveFn(torch.autograd.Function):
         call("clipmi_l2norm_fwd", s, P_(i), P_(ih), P_(inn), B, E)
         tg, ig = _gather(th, group, world), _gather(ih, group, world)
         Bg = tg.shape[0]
-        C = contrastive_chunk()
+        C = contrastive_chunk(world)
         ls = logit_scale.detach().reshape(1)
         lab0 = rank * B
         if Bg > C:

@@ -65,6 +65,15 @@ class GradBucketReducer:
         self._done[id(arena)].append((off, off + n))
         self._issue(arena.grad[off:off + n])
 
+    def reset(self):
+        """Drop this step's bucket bookkeeping (a backward outside train_step, or gradient
+        accumulation, must not leave reported slices behind for the next finish())."""
+        for w in self._works:
+            w.wait()
+        self._works = []
+        for a in self.arenas:
+            self._done[id(a)] = []
+
     def finish(self):
         for a in self.arenas:
             pos = 0
@@ -125,11 +134,27 @@ class FusedAdamW:
             self.reducer = GradBucketReducer(self.arenas, process_group)
 
     def overlap_with(self, model):
-        """Report the model's gradient buckets to this optimizer's reducer during backward."""
-        model.set_grad_hook(self.reducer.ready if self.reducer is not None else None)
+        """Let ``armed_backward`` report the model's gradient buckets to this optimizer's reducer."""
+        self._model = model
         return self
 
+    def armed_backward(self, loss):
+        """loss.backward() with the gradient-ready hook armed for this one backward only: buckets
+        are all-reduced while the lower layers' backward runs, and a backward outside the trainer
+        step (or a second, accumulating one) never issues collectives of its own."""
+        model = getattr(self, "_model", None)
+        if self.reducer is None or model is None:
+            loss.backward()
+            return
+        model.set_grad_hook(self.reducer.ready)
+        try:
+            loss.backward()
+        finally:
+            model.set_grad_hook(None)
+
     def zero_grad(self, set_to_none=False):
+        if self.reducer is not None:
+            self.reducer.reset()
         for a in self.arenas:
             a.zero_grad()
 
@@ -212,7 +237,7 @@ class CLIPAdapterTrainer:
                              pixel_values=batch.get("pixel_values"), return_loss=True)
         loss = outputs["loss"]
         self.optimizer.zero_grad()
-        loss.backward()
+        self.optimizer.armed_backward(loss)
         if self._world() > 1:
             self.optimizer.grads_all_reduce(self.process_group)
         self.optimizer.clip_grad_norm(self.max_grad_norm)
