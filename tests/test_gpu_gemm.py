@@ -240,3 +240,34 @@ def test_layernorm_mxfp8(R, D):
     torch.cuda.synchronize()
     _mx_close(m, ref)
     assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
+
+
+@pytest.mark.parametrize("var", [20, 21])
+@pytest.mark.parametrize("bkm,flags", [
+    (True, _lib.EPI_BIAS), (True, _lib.EPI_BIAS | _lib.EPI_RESID),
+    (True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE), (True, _lib.EPI_BIAS | _lib.EPI_QGELU), (True, 0),
+    (False, 0), (False, _lib.EPI_DQGELU)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 776, 768), (520, 384, 128), (300, 264, 192),
+                                   (2048, 512, 3072)])
+def test_gemm_4wave_matches_pingpong(var, bkm, flags, M, N, K):
+    """4-wave 256x256 kernel (gemm4.hip, 128x128 per wave): same k order of MFMA accumulation as
+    the 8-wave ping-pong kernel, so bitwise-equal outputs (and pre-activations); also within
+    bf16 rounding of a torch fp32 reference."""
+    A = _mk((M, K), torch.bfloat16, 11)
+    B = _mk((N, K) if bkm else (K, N), torch.bfloat16, 12)
+    bias = _mk((N,), torch.bfloat16, 13)
+    res = _mk((M, N), torch.bfloat16, 14)
+    aux0 = _mk((M, N), torch.bfloat16, 15)
+    outs = []
+    for v in (0, var):
+        C = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        aux = aux0.clone()
+        kern.gemm(M, N, K, A, K, True, B, B.stride(0), bkm, C, N, bias=bias, residual=res, ldr=N, aux=aux, ldaux=N,
+                  flags=flags, small_tile=v)
+        outs.append((C, aux))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    acc = A.float() @ (B.float().t() if bkm else B.float())
+    ref, _ = _ref_epi(acc, flags, bias, aux0, res)
+    assert (outs[1][0].float() - ref).abs().max().item() / max(1.0, ref.abs().max().item()) < 3e-2

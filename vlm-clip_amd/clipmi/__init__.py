@@ -11,6 +11,9 @@ def __getattr__(name):
     if name == "CLIPWithAdapters":
         from .model import CLIPWithAdapters
         return CLIPWithAdapters
+    if name == "CLIPTokenizer":  # caption BPE of the input step (dataset.py:152-159)
+        from .tokenizer import CLIPTokenizer
+        return CLIPTokenizer
     if name in ("CLIPAdapterTrainer", "FusedAdamW"):
         from . import trainer
         return getattr(trainer, name)

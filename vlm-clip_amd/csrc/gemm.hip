@@ -30,180 +30,10 @@
 #include <type_traits>
 #include <cstdlib>
 
+#include "gemm_common.h"
+
 namespace {
-
-constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
-constexpr int E8_B = CLIPMI_EPI_BIAS, E8_R = CLIPMI_EPI_RESID, E8_Q = CLIPMI_EPI_QGELU;
-
-struct GemmP {
-  int M, N, K;
-  const void* A; int64_t lda;
-  const void* B; int64_t ldb;
-  void* C; int64_t ldc;
-  const void* bias; const void* res; int64_t ldr;
-  void* aux; int64_t ldaux;
-  float alpha; int flags; int bias_f32;
-  int k_per_split; float* ws;
-  int tiles_n, ntiles;
-  int vec;  // all leading dimensions multiples of 4 elements
-  int var;  // 256-kernel main-loop schedule (0 production)
-  int vec8; // bf16 C with N, ldc/ldr/ldaux multiples of 8 and C/res/aux/bias 16-B aligned
-  int stagger, first_round;  // s_sleep(127) count for half of the first round's workgroups
-  const uint8_t* a_scale; const uint8_t* b_scale;  // MXFP8: E8M0 per 32-element k-block, [rows][K/32]
-  uint8_t* c_scale;                                 // MXFP8 output: E8M0 per 32 columns, [M][N/32]
-  int raster;  // 0: tiles row-major; g > 0: g tile-rows at a time, column by column (tile_coords)
-  float* bws;  // split-K with a fused bias gradient: per-split partial sums [splits][M] (no atomics)
-};
-
-// tile -> (tm, tn).  Row-major, or grouped: g tile-rows at a time, walked column by column, so
-// the ~32 tiles an XCD holds at once (its contiguous share of the XCD-remapped ids) share g A
-// panels and a few B panels in its 4 MB L2 instead of streaming every B panel per tile-row.
-__device__ __forceinline__ void tile_coords(const GemmP& p, int tile, int& tm, int& tn) {
-  if (p.raster > 0) {
-    const int g = p.raster, tiles_m = p.ntiles / p.tiles_n;
-    const int grp = tile / (g * p.tiles_n);
-    const int rem = tile - grp * g * p.tiles_n;
-    const int rows = min(g, tiles_m - grp * g);
-    tn = rem / rows;
-    tm = grp * g + (rem - tn * rows);
-  } else {
-    tm = tile / p.tiles_n;
-    tn = tile - tm * p.tiles_n;
-  }
-}
-
-__device__ __forceinline__ float ld_bias(const GemmP& p, int n) {
-  return p.bias_f32 ? ((const float*)p.bias)[n] : (float)((const bf16*)p.bias)[n];
-}
-
-// v holds C[m][n..n+3] before the epilogue; columns >= N are dropped.  Vector loads and
-// stores when the 4 columns are in range and every leading dimension keeps them aligned.
-template <typename OutT>
-__device__ __forceinline__ void ld4(const OutT* p, float v[4], int nv, bool vec) {
-  if (vec) { load4(p, v); return; }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = j < nv ? to_f32(p[j]) : 0.f;
-}
-template <typename OutT>
-__device__ __forceinline__ void st4(OutT* p, const float v[4], int nv, bool vec) {
-  if (vec) { store4(p, v); return; }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j < nv) p[j] = from_f32<OutT>(v[j]);
-}
-
-template <typename OutT, int EPI>
-__device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[4]) {
-  const int f = EPI >= 0 ? EPI : p.flags;  // EPI >= 0: flags folded at compile time
-  const int nv = min(4, p.N - n);
-  const bool vec = p.vec && nv == 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] *= p.alpha;
-  if (f & CLIPMI_EPI_BIAS) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += j < nv ? ld_bias(p, n + j) : 0.f;
-  }
-  if (f & CLIPMI_EPI_STORE_PRE) st4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v, nv, vec);
-  if (f & CLIPMI_EPI_QGELU) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
-  } else if (f & CLIPMI_EPI_GELU) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
-  }
-  if (f & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)) {
-    float a[4];
-    ld4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, a, nv, vec);
-    if (f & CLIPMI_EPI_DQGELU) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] *= quick_gelu_grad(a[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] *= gelu_erf_grad(a[j]);
-    }
-  }
-  if (f & CLIPMI_EPI_RESID) {
-    float r[4];
-    ld4((const OutT*)p.res + (int64_t)m * p.ldr + n, r, nv, vec);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += r[j];
-  }
-  OutT* c = (OutT*)p.C + (int64_t)m * p.ldc + n;
-  if (f & CLIPMI_EPI_BETA) {
-    float o[4];
-    ld4(c, o, nv, vec);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += o[j];
-  }
-  st4(c, v, nv, vec);
-}
-
-// ---------------------------------------------------------------- LDS images
-// k-major image: [128 rows][64 k] bf16, 128-B rows, 16-B chunk c stored at c ^ ((r>>1)&7)
-__device__ __forceinline__ int kimg_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-// row-major-in-k image: [64 k][128 rows] bf16, 256-B rows, chunk c stored at c ^ 2*g(r)
-__device__ __forceinline__ int mimg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
-__device__ __forceinline__ int mimg_off(int r, int c) { return r * 256 + ((c ^ mimg_swz(r)) << 4); }
-
-// Global -> register staging of one 128x64 operand tile (4 x 16 B per thread).
-template <bool KMAJ>
-struct Stager {
-  const bf16* base[4];  // per pass: k-major -> row start (+chunk), else column chunk start
-  int lds_off[4];
-  int chunk_k[4];       // k-major: element offset of the chunk within the K step; else k row
-  __device__ __forceinline__ void init(const bf16* X, int64_t ld, int row0, int R, int t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int id = i * NTHR + t;
-      if (KMAJ) {
-        int r = id >> 3, c = id & 7;
-        int gr = min(row0 + r, R - 1);
-        base[i] = X + (int64_t)gr * ld + c * 8;
-        chunk_k[i] = c * 8;
-        lds_off[i] = kimg_off(r, c);
-      } else {
-        int kr = id >> 4, c = id & 15;
-        int gc = min(row0 + c * 8, R - 8);
-        base[i] = X + (int64_t)kr * ld + gc;
-        chunk_k[i] = kr;
-        lds_off[i] = mimg_off(kr, c);
-      }
-    }
-  }
-  __device__ __forceinline__ void load(u32x4 v[4], int k0, int64_t ld, int kvalid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16* g = KMAJ ? base[i] + k0 : base[i] + (int64_t)k0 * ld;
-      if (kvalid >= BK || chunk_k[i] < kvalid) v[i] = *(const u32x4*)g;
-      else v[i] = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, const u32x4 v[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *LDS_PTR(u32x4, lds + lds_off[i]) = v[i];
-  }
-};
-
-// One 16x32 MFMA operand fragment: rows rb..rb+15 of the tile, k = kk*32 .. kk*32+31.
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int kk, int lane) {
-  if (KMAJ) {
-    int r = rb + (lane & 15), c = kk * 4 + (lane >> 4);
-    return *LDS_PTR(const bf16x8, lds + kimg_off(r, c));
-  } else {
-    int q = (lane & 15) >> 2, p4 = lane & 3;
-    int m = rb + 4 * p4;
-    int r0 = kk * 32 + 8 * (lane >> 4) + q;
-    int r1 = r0 + 4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        LDS_PTR(s16x4, lds + mimg_off(r0, m >> 3) + (m & 7) * 2));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        LDS_PTR(s16x4, lds + mimg_off(r1, m >> 3) + (m & 7) * 2));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, w);
-  }
-}
+using namespace cmg;
 
 template <bool AK, bool BKM, typename OutT, int EPI>
 __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
@@ -286,389 +116,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_kernel(GemmP p) {
       } else {
         epilogue4<OutT, EPI>(p, m, n, v);
       }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ 256x256 LDS-DMA path
-// 512 threads = 8 waves (2 along M x 4 along N), each wave 128x64 = 8x4 MFMA tiles
-// (128 accumulator VGPRs).  Tiles arrive by LDS-DMA (buffer_load ... lds, 16 B per lane,
-// 1 KiB per wave-instruction): the LDS images are lane-linear, so the XOR swizzle is
-// applied to the per-lane SOURCE address and undone by the same read-side swizzle as the
-// 128 kernel.  Two 64 KiB buffers: the DMA of k-step t+1 is in flight while k-step t's
-// 64 MFMAs per wave run; one vmcnt(0) + barrier per k-step.  Buffer descriptors are
-// rebuilt per k-step at the slab start with exact byte extents, so rows past M/N/K read
-// as zero (no clamping, no branches) and offsets stay 32-bit for any tensor size.
-// BIASGRAD (wgrad only): waves with wn == 0 of n-tile 0 add one MFMA per A fragment
-// against a ones fragment, producing sum_k A(m,k) = the Linear bias gradient.
-constexpr int BT = 256, NT2 = 512;
-
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, int voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0, 0);
-}
-// stage one 256x64 operand tile of k-step at k0 into an LDS image (32 KiB)
-template <bool KMAJ>
-__device__ __forceinline__ void stage256(char* img, const bf16* X, int64_t ld, int row0, int R, int k0, int K,
-                                         int wave, int lane) {
-  if (KMAJ) {
-    // rows row0.. (<=256 valid), k0..k0+63; each wave-instruction fills 8 rows x 128 B
-    const int rows = min(BT, R - row0);
-    const bf16* base = X + (int64_t)row0 * ld + k0;
-    const uint32_t rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
-    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = wave * 4 + i;
-      const int r = 8 * j + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      dma16(rs, img + j * 1024, (int)((int64_t)r * ld * 2 + c * 16));
-    }
-  } else {
-    // k rows k0..k0+63 (<= K), columns row0..row0+255 as two 128-wide half images [64][128]
-    const int krows = min(64, K - k0);
-    const int cols = min(BT, R - row0);
-    const bf16* base = X + (int64_t)k0 * ld + row0;
-    const uint32_t rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
-    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = wave * 4 + i;            // 0..31
-      const int half = j >> 4;
-      const int kr = 4 * (j & 15) + (lane >> 4);
-      const int c = (lane & 15) ^ mimg_swz(kr);
-      dma16(rs, img + half * 16384 + (j & 15) * 1024, (int)((int64_t)kr * ld * 2 + (half * 128 + c * 8) * 2));
-    }
-  }
-}
-
-// issue DMA instruction i (0..3) of this wave for one operand tile (same addressing as stage256)
-template <bool KMAJ, typename RS>
-__device__ __forceinline__ void stage256_one(char* img, RS rs, int64_t ld, int wave, int lane, int i) {
-  const int j = wave * 4 + i;
-  if (KMAJ) {
-    const int r = 8 * j + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    dma16(rs, img + j * 1024, (int)((int64_t)r * ld * 2 + c * 16));
-  } else {
-    const int half = j >> 4;
-    const int kr = 4 * (j & 15) + (lane >> 4);
-    const int c = (lane & 15) ^ mimg_swz(kr);
-    dma16(rs, img + half * 16384 + (j & 15) * 1024, (int)((int64_t)kr * ld * 2 + (half * 128 + c * 8) * 2));
-  }
-}
-template <bool KMAJ>
-__device__ __forceinline__ void extent256(const bf16* X, int64_t ld, int row0, int R, int k0, int K, const bf16*& base,
-                                          uint32_t& rec) {
-  if (KMAJ) {
-    const int rows = min(BT, R - row0);
-    base = X + (int64_t)row0 * ld + k0;
-    rec = rows > 0 ? (uint32_t)((int64_t)(rows - 1) * ld * 2 + 128) : 0u;
-  } else {
-    const int krows = min(64, K - k0);
-    const int cols = min(BT, R - row0);
-    base = X + (int64_t)k0 * ld + row0;
-    rec = krows > 0 ? (uint32_t)((int64_t)(krows - 1) * ld * 2 + (int64_t)cols * 2) : 0u;
-  }
-}
-template <bool KMAJ>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
-  const bf16* base; uint32_t rec;
-  extent256<KMAJ>(X, ld, row0, R, k0, K, base, rec);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rec, 0x00020000);
-}
-template <bool KMAJ>
-__device__ __forceinline__ SRsrc srsrc256(const bf16* X, int64_t ld, int row0, int R, int k0, int K) {
-  const bf16* base; uint32_t rec;
-  extent256<KMAJ>(X, ld, row0, R, k0, K, base, rec);
-  return make_srsrc(base, rec);
-}
-
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 read_frag256(const char* img, int rb, int kk, int lane) {
-  if (KMAJ) return read_frag<true>(img, rb, kk, lane);
-  return read_frag<false>(img + (rb >> 7) * 16384, rb & 127, kk, lane);
-}
-
-// Batched epilogue for the 256 kernel (vectorisable case): bias preloaded once per lane,
-// residual / pre-activation / old-C vectors for half the tile loaded in one burst (clamped
-// addresses, no per-element branches), then computed and stored.  The per-subtile
-// load->wait->store chain it replaces left the K=768 GEMMs epilogue-latency bound.
-template <typename OutT, int EPI>
-__device__ __forceinline__ void epilogue256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
-  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
-  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
-  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
-  constexpr bool HAUX = HDQ || HDG;
-  const int nlane = (lane >> 4) * 4, mlane = lane & 15;
-  float bv[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = min(nb + j * 16 + nlane, p.N - 4);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
-    if (HB) {
-      if (p.bias_f32) load4((const float*)p.bias + n, bv[j]);
-      else load4((const bf16*)p.bias + n, bv[j]);
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float xin[4][4][4];
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = min(nb + j * 16 + nlane, p.N - 4);
-        if (HR) load4((const OutT*)p.res + (int64_t)m * p.ldr + n, xin[ii][j]);
-        else if (HAUX) load4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][j]);
-        else if (HBETA) load4((const OutT*)p.C + (int64_t)m * p.ldc + n, xin[ii][j]);
-      }
-    }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = h * 4 + ii;
-      const int m = mb + i * 16 + mlane;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = nb + j * 16 + nlane;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[i][j][r] * p.alpha + bv[j][r];
-        }
-        const bool ok = m < p.M && n < p.N;
-        if (HPRE && ok) store4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (HQ) v[r] = quick_gelu(v[r]);
-          if (HG) v[r] = gelu_erf(v[r]);
-          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][j][r]);
-          if (HDG) v[r] *= gelu_erf_grad(xin[ii][j][r]);
-          if (HR || HBETA) v[r] += xin[ii][j][r];
-        }
-        if (ok) store4((OutT*)p.C + (int64_t)m * p.ldc + n, v);
-      }
-    }
-  }
-}
-
-// 8 consecutive bf16 as float (one 16-B access)
-__device__ __forceinline__ void load8(const bf16* p, float v[8]) {
-  const bf16x8 t = *(const bf16x8*)p;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) v[r] = (float)t[r];
-}
-__device__ __forceinline__ void store8(bf16* p, const float v[8]) {
-  *(bf16x8*)p = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
-}
-
-// bf16-output epilogue with 16-B accesses (cdna_hip_programming.md T21, 16-lane form).  The
-// 16x16 accumulator layout gives a lane 4 consecutive columns per fragment, i.e. 8-B stores of
-// 16 rows x 32 B per instruction, and those epilogues were store-issue bound.  One
-// v_permlane16_swap per accumulator dword pairs fragments (2jp, 2jp+1): afterwards lane
-// row-group q = lane>>4 holds 8 consecutive columns, fragment 2jp + (q & 1), columns
-// 8*(q >> 1) .. +7, so every residual/aux load and every store is one 16-B access covering
-// 16 rows x 64 B per instruction: half the memory instructions for the same bytes.
-template <int EPI>
-__device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
-  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
-  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
-  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
-  constexpr bool HAUX = HDQ || HDG;
-  const int q = lane >> 4, mlane = lane & 15;
-  const int coff = 16 * (q & 1) + 8 * (q >> 1);  // this lane's column within a fragment pair
-  float bv[2][8];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    const int n = min(nb + 32 * jp + coff, p.N - 8);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
-    if (HB) {
-      if (p.bias_f32) {
-        load4((const float*)p.bias + n, bv[jp]);
-        load4((const float*)p.bias + n + 4, bv[jp] + 4);
-      } else {
-        load8((const bf16*)p.bias + n, bv[jp]);
-      }
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float xin[4][2][8];
-    if (HR || HAUX || HBETA) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const int n = min(nb + 32 * jp + coff, p.N - 8);
-          if (HR) load8((const bf16*)p.res + (int64_t)m * p.ldr + n, xin[ii][jp]);
-          else if (HAUX) load8((const bf16*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][jp]);
-          else load8((const bf16*)p.C + (int64_t)m * p.ldc + n, xin[ii][jp]);
-        }
-      }
-    }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = h * 4 + ii;
-      const int m = mb + i * 16 + mlane;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        const int n = nb + 32 * jp + coff;
-        float v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {  // swapped right before use: no extra live registers
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
-                                                           __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
-          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
-          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
-        }
-        const bool ok = m < p.M && n < p.N;
-        if (HPRE && ok) store8((bf16*)p.aux + (int64_t)m * p.ldaux + n, v);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          if (HQ) v[r] = quick_gelu(v[r]);
-          if (HG) v[r] = gelu_erf(v[r]);
-          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][jp][r]);
-          if (HDG) v[r] *= gelu_erf_grad(xin[ii][jp][r]);
-          if (HR || HBETA) v[r] += xin[ii][jp][r];
-        }
-        if (ok) store8((bf16*)p.C + (int64_t)m * p.ldc + n, v);
-      }
-    }
-  }
-}
-
-// Full-line stores through LDS: the values of epilogue256_w (same math, same loads) are written
-// to the wave's 16 KiB LDS region as a [128 rows][64 cols] bf16 tile (16-B chunk c of row r at
-// c ^ (r & 7): conflict-free 8-lane writes and 16-lane reads), then read back row-contiguous so
-// each global store instruction covers 8 whole 128-B rows instead of 16 rows x 64 B.  Needs
-// the ring idle (after the kernel's final barrier) and is used for the pre-activation store too.
-__device__ __forceinline__ int stage_off(int r, int c8) { return r * 128 + ((c8 ^ (r & 7)) << 4); }
-
-__device__ __forceinline__ void stage_store_rows(const GemmP& p, const char* st, bf16* out, int64_t ld, int mb, int nb,
-                                                 int lane) {
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {  // 64 rows, 8 whole rows per instruction
-    const int r = it * 8 + (lane >> 3), c8 = lane & 7;
-    const u32x4 v = *LDS_PTR(const u32x4, st + stage_off(r, c8));
-    const int m = mb + r, n = nb + c8 * 8;
-    if (m < p.M && n < p.N) *(u32x4*)(out + (int64_t)m * ld + n) = v;
-  }
-}
-
-template <int EPI>
-__device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane,
-                                                char* st) {
-  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
-  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
-  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
-  constexpr bool HAUX = HDQ || HDG;
-  const int q = lane >> 4, mlane = lane & 15;
-  const int coff = 16 * (q & 1) + 8 * (q >> 1);
-  char* st_out = st;  // [64 rows][64 cols] bf16 = 8 KiB per half of the wave's rows
-  float bv[2][8];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    const int n = min(nb + 32 * jp + coff, p.N - 8);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
-    if (HB) {
-      if (p.bias_f32) {
-        load4((const float*)p.bias + n, bv[jp]);
-        load4((const float*)p.bias + n + 4, bv[jp] + 4);
-      } else {
-        load8((const bf16*)p.bias + n, bv[jp]);
-      }
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float xin[4][2][8];
-    if (HR || HAUX || HBETA) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const int n = min(nb + 32 * jp + coff, p.N - 8);
-          if (HR) load8((const bf16*)p.res + (int64_t)m * p.ldr + n, xin[ii][jp]);
-          else if (HAUX) load8((const bf16*)p.aux + (int64_t)m * p.ldaux + n, xin[ii][jp]);
-          else load8((const bf16*)p.C + (int64_t)m * p.ldc + n, xin[ii][jp]);
-        }
-      }
-    }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = h * 4 + ii;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        float v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
-                                                           __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
-          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
-          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
-        }
-        const int off = stage_off(ii * 16 + mlane, (32 * jp + coff) >> 3);
-        if (HPRE) {  // the pre-activation goes out directly (16 rows x 64 B), overlapping the gelu math
-          const int m = mb + i * 16 + mlane, n = nb + 32 * jp + coff;
-          if (m < p.M && n < p.N) store8((bf16*)p.aux + (int64_t)m * p.ldaux + n, v);
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          if (HQ) v[r] = quick_gelu(v[r]);
-          if (HG) v[r] = gelu_erf(v[r]);
-          if (HDQ) v[r] *= quick_gelu_grad(xin[ii][jp][r]);
-          if (HDG) v[r] *= gelu_erf_grad(xin[ii][jp][r]);
-          if (HR || HBETA) v[r] += xin[ii][jp][r];
-        }
-        *LDS_PTR(bf16x8, st_out + off) = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
-                                                (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staging writes landed
-    stage_store_rows(p, st_out, (bf16*)p.C, p.ldc, mb + h * 64, nb, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next half overwrites
-  }
-}
-
-// Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
-// allows it (4-aligned columns, aligned leading dims; the 16-B form for bf16 output when
-// columns, leading dims and pointers allow 16-B accesses), else the per-subtile generic path
-// (split-K slab kz, ragged N, runtime flags).
-template <typename OutT, int EPI>
-__device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane, int kz,
-                                          char* stage = nullptr) {
-  constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
-                        !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
-  if constexpr (FAST && std::is_same<OutT, bf16>::value) {
-    if (stage && !p.ws && p.vec8) {
-      epilogue256_lds<EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane, stage);
-      return;
-    }
-    if (!p.ws && p.vec8) {
-      epilogue256_w<EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
-      return;
-    }
-  }
-  if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
-    epilogue256<OutT, EPI < 0 ? 0 : EPI>(p, acc, mb, nb, lane);
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mb + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = nb + j * 16 + (lane >> 4) * 4;
-      if (n >= p.N) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.ws) st4(p.ws + (int64_t)kz * p.M * p.N + (int64_t)m * p.N + n, v, min(4, p.N - n), p.vec && n + 4 <= p.N);
-      else epilogue4<OutT, EPI>(p, m, n, v);
     }
   }
 }
@@ -1810,6 +1257,9 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     return "gemm256_wgrad";
   }
   if (bg) return nullptr;
+  if ((p.var == 20 || p.var == 21) && !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
+    if (const char* l = dispatch_w4(p, s, sel == 3, flags, p.var == 21 ? 2 : 1)) return l;
+  }
   if (sel == 3 && !f32o) {
     switch (flags) {
       case E_B: launch256<true, true, bf16, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias";
