@@ -77,6 +77,10 @@ typedef struct clipmi_gemm_desc {
 #define CLIPMI_EPI_STORE_PRE 128
 
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
+/* Diagnostic (no reference counterpart): arm / disarm (nullptr) the in-kernel s_memtime stamps of
+ * the 4-wave GEMM's timing variant (force_small_tile = 22); buf holds 512 * 4 * 128 u64 of device
+ * memory (layout: csrc/gemm4.hip, reader: tools/w4_stamps.py). */
+int clipmi_gemm_stamps(void* buf);
 /* MXFP8 quantisation of a [R, K] bf16/f32 matrix (row stride ldx elements) into OCP e4m3 bytes
  * q [R, K] and E8M0 block scales [R, K/32]: per 32-element block the smallest power of two that
  * brings the block's max |x| to <= 448, round-to-nearest-even. */

@@ -242,7 +242,7 @@ def test_layernorm_mxfp8(R, D):
     assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
 
 
-@pytest.mark.parametrize("var", [20, 21])
+@pytest.mark.parametrize("var", [20, 21, 28, 29])
 @pytest.mark.parametrize("bkm,flags", [
     (True, _lib.EPI_BIAS), (True, _lib.EPI_BIAS | _lib.EPI_RESID),
     (True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE), (True, _lib.EPI_BIAS | _lib.EPI_QGELU), (True, 0),

@@ -26,6 +26,9 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("t_fc1_fwd", RT, 2048, 512, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("t_fc2_fwd", RT, 512, 2048, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
     ("t_qkv_fwd", RT, 1536, 512, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
+    ("t_fc2_dgrad", RT, 2048, 512, True, False, torch.bfloat16, _lib.EPI_DQGELU, 1),
+    ("t_fc1_dgrad", RT, 512, 2048, True, False, torch.bfloat16, 0, 1),
+    ("t_qkv_dgrad", RT, 512, 1536, True, False, torch.bfloat16, 0, 1),
     # the same shapes with K = 64: prologue + epilogue cost per tile
     ("fc1_k64", R, 3072, 64, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("qkv_k64", R, 2304, 64, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),

@@ -173,6 +173,33 @@ def gen_b16_full_grads():
     save("forward_b16_full_grads.npz", **out)
 
 
+def gen_b16_feature_grads():
+    """Config 3's backward in a well-conditioned form: ViT-B/16 full fine-tune, B = 4, the reference's
+    own feature paths (model_m.py:77-125: text = adapter-free tower -> token 0 -> text_projection,
+    quirk Q1; image = CLS without post-LN, quirk Q2), L = <text_features, Gt> + <image_features, Gi>
+    with fixed random Gt, Gi (no contrastive softmax, whose B = 2 logits nearly cancel).  Every
+    parameter's gradient, sampled as in gen_b16_full_grads."""
+    cfg = C.resolve("B/16")
+    ref = build_reference_model(cfg, False, False, freeze_clip=False)
+    b_np, b = batch_tensors(cfg, 4)
+    ref.train()
+    tf = ref.get_text_features(b["input_ids"], b["attention_mask"])
+    imf = ref.get_image_features(b["pixel_values"])
+    Gt = torch.from_numpy(synth.normal(tuple(tf.shape), 31, "featgrad_Gt"))
+    Gi = torch.from_numpy(synth.normal(tuple(imf.shape), 31, "featgrad_Gi"))
+    ((tf * Gt).sum() + (imf * Gi).sum()).backward()
+    out = {"input_digest": np.array(digest(b_np["pixel_values"], b_np["input_ids"], b_np["attention_mask"])),
+           "G_digest": np.array(digest(Gt.numpy(), Gi.numpy())),
+           "text_features": tf.detach().numpy(), "image_features": imf.detach().numpy()}
+    n = 0
+    for k, p in ref.named_parameters():
+        if p.grad is not None:
+            out.update(_grad_sample(k[5:] if k.startswith("clip.") else k, p.grad.numpy(), b_np["input_ids"]))
+            n += 1
+    print("b16 feature grads: tensors", n)
+    save("forward_b16_feature_grads.npz", **out)
+
+
 def gen_b32_adapter_b256():
     """BASELINE config 2's batch at parity: ViT-B/32 + text/vision adapters (A=256, shared off), frozen
     towers, B=256: features, logits, loss and the adapter gradients (the trainable set)."""
@@ -506,3 +533,4 @@ if __name__ == "__main__":
     gen_l14()
     gen_heads()
     gen_shared()
+    gen_b16_feature_grads()

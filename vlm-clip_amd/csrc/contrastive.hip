@@ -10,7 +10,11 @@
 // the ranks' losses is the single-device loss.  logit_scale stays on the device (it is
 // trainable in full fine-tune), so no host synchronisation happens anywhere.
 // The [B, Bg] cosine blocks come from the f32 GEMM (exact f32); these kernels do the
-// per-row softmax statistics.  All contrastive arithmetic is fp32.
+// per-row softmax statistics.  All contrastive arithmetic is fp32, with the accurate expf / logf
+// (not the 1-2 ulp __expf / __logf): at small B the loss gradient is a difference of nearly
+// equal softmax terms (config 3 at B = 2: text rows identical under quirk Q1, p ~ 0.5), and
+// the fast forms amplified to ~1e-3 relative error in every vision gradient; this head is < 1 %
+// of a step.
 #include "common.h"
 #include "internal.h"
 
@@ -50,17 +54,17 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* S, float* L, c
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
-  const float sc = __expf(*logit_scale);
+  const float sc = expf(*logit_scale);
   const float* s = S + (int64_t)row * Bg;
   float* l = L + (int64_t)row * Bg;
   float mx = -__builtin_huge_valf();
   for (int j = lane; j < Bg; j += 64) { float v = s[j] * sc; l[j] = v; mx = fmaxf(mx, v); }
   mx = wave_max(mx);
   float sum = 0.f;
-  for (int j = lane; j < Bg; j += 64) sum += __expf(l[j] - mx);
+  for (int j = lane; j < Bg; j += 64) sum += expf(l[j] - mx);
   sum = wave_sum(sum);
   if (lane == 0) {
-    const float lse = mx + __logf(sum);
+    const float lse = mx + logf(sum);
     lse_out[row] = lse;
     ce_out[row] = lse - l[label0 + row];
   }
@@ -73,14 +77,14 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* L, const float
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
-  const float sc = __expf(*logit_scale);
+  const float sc = expf(*logit_scale);
   const float g = (gout ? *gout : 1.f) * norm;
   const float* l = L + (int64_t)row * Bg;
   float* d = dS + (int64_t)row * Bg;
   const float ls = lse[row];
   float acc = 0.f;
   for (int j = lane; j < Bg; j += 64) {
-    float dl = g * (__expf(l[j] - ls) - (j == label0 + row ? 1.f : 0.f));
+    float dl = g * (expf(l[j] - ls) - (j == label0 + row ? 1.f : 0.f));
     acc += dl * l[j];
     d[j] = dl * sc;
   }
@@ -99,13 +103,13 @@ __global__ __launch_bounds__(256) void ce_fwd_chunk_kernel(const float* S, const
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
-  const float sc = __expf(*logit_scale);
+  const float sc = expf(*logit_scale);
   const float* s = S + (int64_t)row * C;
   float mx = -__builtin_huge_valf();
   for (int j = lane; j < C; j += 64) mx = fmaxf(mx, s[j] * sc);
   mx = wave_max(mx);
   float sum = 0.f;
-  for (int j = lane; j < C; j += 64) sum += __expf(s[j] * sc - mx);
+  for (int j = lane; j < C; j += 64) sum += expf(s[j] * sc - mx);
   sum = wave_sum(sum);
   if (lane == 0) {
     float* r = run + 2 * (int64_t)row;
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(256) void ce_fwd_chunk_kernel(const float* S, const
       r[1] = sum;
     } else {
       const float m = fmaxf(r[0], mx);
-      r[1] = r[1] * __expf(r[0] - m) + sum * __expf(mx - m);
+      r[1] = r[1] * expf(r[0] - m) + sum * expf(mx - m);
       r[0] = m;
     }
     const int lc = label0 + row - col0;
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(256) void ce_finish_kernel(const float* run, const 
                                                         float* ce_out) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= B) return;
-  const float lse = run[2 * row] + __logf(run[2 * row + 1]);
+  const float lse = run[2 * row] + logf(run[2 * row + 1]);
   lse_out[row] = lse;
   ce_out[row] = lse - lab[row];
 }
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(256) void ce_bwd_chunk_kernel(const float* S, const
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
-  const float sc = __expf(*logit_scale);
+  const float sc = expf(*logit_scale);
   const float g = (gout ? *gout : 1.f) * norm;
   const float* s = S + (int64_t)row * C;
   float* d = dS + (int64_t)row * C;
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(256) void ce_bwd_chunk_kernel(const float* S, const
   float acc = 0.f;
   for (int j = lane; j < C; j += 64) {
     const float l = s[j] * sc;
-    const float dl = g * (__expf(l - ls) - (j == lc ? 1.f : 0.f));
+    const float dl = g * (expf(l - ls) - (j == lc ? 1.f : 0.f));
     acc += dl * l;
     d[j] = dl * sc;
   }

@@ -1257,8 +1257,20 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     return "gemm256_wgrad";
   }
   if (bg) return nullptr;
-  if ((p.var == 20 || p.var == 21) && !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
-    if (const char* l = dispatch_w4(p, s, sel == 3, flags, p.var == 21 ? 2 : 1)) return l;
+  // 20 / 21: 4-wave kernel (DMAs spread / front-loaded); 22-25: its stamped timing builds
+  // (22 production schedule, 23 no main-loop DMAs, 24 no fragment reads, 25 neither, 26 one M0 write
+  // per half-step: wrong LDS targets, timing only; 27 32x32x16 MFMAs on the same reads, timing only)
+  // 28-30: the persistent 4-wave kernel (stagger 0 / 4 / 8 x s_sleep 127 for half of each XCD's CUs)
+  // production (var 0): the persistent 4-wave kernel for long-K products (K >= 1536), where its main
+  // loop is 3-7 % faster than the ping-pong kernel's; at K = 768 / 512 the ping-pong kernel's 8 waves
+  // run the VALU-heavy epilogues twice as fast per SIMD (tools/w4_stamps.py, profiles/r03_*)
+  const bool w4_default = p.var == 0 && p.K >= 1536;
+  if ((w4_default || p.var == 20 || p.var == 21 || (p.var >= 22 && p.var <= 27 && p.dbg) || (p.var >= 28 && p.var <= 30)) &&
+      !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
+    GemmP q = p;
+    if (p.var >= 28) q.stagger = (p.var - 28) * 4;
+    const int dm = p.var == 21 ? 2 : (p.var >= 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
+    if (const char* l = dispatch_w4(q, s, sel == 3, flags, dm)) return l;
   }
   if (sel == 3 && !f32o) {
     switch (flags) {
@@ -1341,6 +1353,20 @@ int raster_rows(bool fp8 = false) {
 
 }  // namespace
 
+namespace cmg {
+static unsigned long long* g_stamps = nullptr;
+unsigned long long* gemm_stamp_buffer() { return g_stamps; }
+}  // namespace cmg
+
+// Diagnostic: arm (buf != nullptr) or disarm the 4-wave kernel's in-kernel timing build (variant
+// 22): per workgroup < 512 and wave, s_memtime/s_memrealtime stamps of kernel start, main-loop
+// start/end, kernel end and every k-step's barrier (before/after), 128 u64 per wave
+// (tools/w4_stamps.py).  buf: device memory of 512 * 4 * 128 u64.
+extern "C" int clipmi_gemm_stamps(void* buf) {
+  cmg::g_stamps = (unsigned long long*)buf;
+  return CLIPMI_OK;
+}
+
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
@@ -1418,6 +1444,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   const bool wlayout = !d->a_kmajor && !d->b_kmajor;
   const int evar = wlayout ? env_wvar : env_var;
   p.raster = raster_rows();
+  p.dbg = gemm_stamp_buffer();
   p.stagger = 0;
   p.first_round = num_cus();
   if (d->force_small_tile >= 100) {  // A/B hook: 1xx ping-pong, 2xx persistent, with a stagger of xx

@@ -30,7 +30,11 @@ struct GemmP {
   uint8_t* c_scale;                                 // MXFP8 output: E8M0 per 32 columns, [M][N/32]
   int raster;  // 0: tiles row-major; g > 0: g tile-rows at a time, column by column (tile_coords)
   float* bws;  // split-K with a fused bias gradient: per-split partial sums [splits][M] (no atomics)
+  unsigned long long* dbg;  // diagnostic builds only: in-kernel s_memtime stamps (clipmi_gemm_stamps)
 };
+
+// host side: the stamp buffer armed by clipmi_gemm_stamps (nullptr when disarmed)
+unsigned long long* gemm_stamp_buffer();
 
 // tile -> (tm, tn).  Row-major, or grouped: g tile-rows at a time, walked column by column, so
 // the ~32 tiles an XCD holds at once (its contiguous share of the XCD-remapped ids) share g A
