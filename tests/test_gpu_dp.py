@@ -14,6 +14,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False):
+    try:
+        _worker_body(rank, world, port, q, overlap, chunk, shared)
+    except BaseException:  # report instead of leaving the parent waiting on the queue
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+        raise
+
+
+def _worker_body(rank, world, port, q, overlap, chunk, shared):
     import sys
     if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
         os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
@@ -24,9 +33,13 @@ def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    m = CLIPWithAdapters("tiny", use_text_adapter=True, use_vision_adapter=True, use_shared_adapters=shared,
+    # shared adapters need text hidden 512 (their text_projection, model_m.py:54-61): B/32
+    m = CLIPWithAdapters("B/32" if shared else "tiny", use_text_adapter=True, use_vision_adapter=True,
+                         use_shared_adapters=shared,
                          freeze_clip=False, device="cuda:0", precision="fp32", pooling="eos",
                          process_group=dist.group.WORLD)
+    if shared:
+        m.eval()  # shared-adapter dropout off: the ranks must reproduce the single-device gradients
     B = 4
     b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
     if overlap:  # gradient buckets all-reduced from the towers' chunked backward (GradBucketReducer)
@@ -59,11 +72,21 @@ def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk, shared)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    res = []
+    for _ in procs:
+        r = q.get(timeout=200)
+        if r[1] is None:  # a rank failed: its partner may be stuck in a collective
+            for p in procs:
+                p.kill()
+            raise AssertionError(f"rank {r[0]} failed:\n{r[2]}")
+        res.append(r)
+    res.sort(key=lambda x: x[0])
     for p in procs:
         p.join(120)
-    m = CLIPWithAdapters("tiny", use_shared_adapters=shared, freeze_clip=False, device="cuda:0", precision="fp32",
-                         pooling="eos")
+    m = CLIPWithAdapters("B/32" if shared else "tiny", use_shared_adapters=shared, freeze_clip=False, device="cuda:0",
+                         precision="fp32", pooling="eos")
+    if shared:
+        m.eval()
     b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, 8, seed=5).items()}
     out = m(**b)
     out["loss"].backward()
