@@ -34,8 +34,7 @@ for name in sys.argv[1:] or ["fc1_dgrad"]:
     f = lambda v: K.gemm(M, N, Kd, A, Kd, True, B, Kd if bkm else N, bkm, C, N, small_tile=v, **kw)
     for _ in range(3):
         f(20)
-    for var, what in ((22, "production"), (23, "no main-loop DMAs"), (24, "no fragment reads"), (25, "MFMAs only"),
-                      (26, "DMAs without per-piece M0 writes"), (27, "32x32x16 MFMAs")):
+    for var, what in ((22, "production"), (23, "no main-loop DMAs"), (24, "no fragment reads"), (25, "MFMAs only")):
         L.clipmi_gemm_stamps(ctypes.c_void_p(buf.data_ptr()))
         f(var)
         torch.cuda.synchronize()

@@ -1247,6 +1247,9 @@ constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU, E_DG = CLIPM
 
 const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
   if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
+    if (p.var == 28) {  // the persistent 4-wave kernel (gemm4.hip)
+      if (const char* l = dispatch_w4_wgrad(p, splits, s, flags, bg)) return l;
+    }
     if (p.ws) {
       if (bg) launch256<false, false, float, 0, true>(p, splits, s, bg);
       else launch256<false, false, float, 0, false>(p, splits, s, bg);
@@ -1257,19 +1260,18 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     return "gemm256_wgrad";
   }
   if (bg) return nullptr;
-  // 20 / 21: 4-wave kernel (DMAs spread / front-loaded); 22-25: its stamped timing builds
-  // (22 production schedule, 23 no main-loop DMAs, 24 no fragment reads, 25 neither, 26 one M0 write
-  // per half-step: wrong LDS targets, timing only; 27 32x32x16 MFMAs on the same reads, timing only)
+  // 20: 4-wave kernel, one tile per workgroup; 22-25: its stamped timing builds (22 production
+  // schedule, 23 no main-loop DMAs, 24 no fragment reads, 25 neither)
   // 28-30: the persistent 4-wave kernel (stagger 0 / 4 / 8 x s_sleep 127 for half of each XCD's CUs)
   // production (var 0): the persistent 4-wave kernel for long-K products (K >= 1536), where its main
   // loop is 3-7 % faster than the ping-pong kernel's; at K = 768 / 512 the ping-pong kernel's 8 waves
   // run the VALU-heavy epilogues twice as fast per SIMD (tools/w4_stamps.py, profiles/r03_*)
   const bool w4_default = p.var == 0 && p.K >= 1536;
-  if ((w4_default || p.var == 20 || p.var == 21 || (p.var >= 22 && p.var <= 27 && p.dbg) || (p.var >= 28 && p.var <= 30)) &&
+  if ((w4_default || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || (p.var >= 28 && p.var <= 30)) &&
       !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
     GemmP q = p;
     if (p.var >= 28) q.stagger = (p.var - 28) * 4;
-    const int dm = p.var == 21 ? 2 : (p.var >= 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
+    const int dm = (p.var >= 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
     if (const char* l = dispatch_w4(q, s, sel == 3, flags, dm)) return l;
   }
   if (sel == 3 && !f32o) {
@@ -1452,7 +1454,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     p.stagger = d->force_small_tile % 100;
   } else if (d->force_small_tile >= 2) p.var = d->force_small_tile;
   else if (evar >= 0 && d->force_small_tile == 0) p.var = evar;
-  else p.var = wlayout ? 4 : 0;
+  else p.var = wlayout ? 28 : 0;  // wgrad: the persistent 4-wave kernel (5-11 % over var 4, profiles/r03_wgrad_4wave.log)
   p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
           ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
   p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&

@@ -1,27 +1,35 @@
-// 4-wave 256x256 bf16 GEMM for the forward / dgrad layouts (one wave per SIMD).
+// 4-wave 256x256 bf16 GEMM (one wave per SIMD): forward, dgrad and weight-gradient layouts.
 //
-// Replaces the same nn.Linear products as gemm.hip's ping-pong kernel ([HF] modeling_clip.py
-// :313-315,332 q/k/v/out_proj, :348-350 fc1/fc2 and their input gradients) with a schedule
-// built around one wave per SIMD instead of two:
+// Replaces the same nn.Linear products as gemm.hip's 8-wave kernels ([HF] modeling_clip.py
+// :313-315,332 q/k/v/out_proj, :348-350 fc1/fc2, their input gradients and their weight / bias
+// gradients, i.e. the reference's loss.backward through those layers, trainer.py:92) with a
+// schedule built around one wave per SIMD instead of two:
 //  * 256 threads, 4 waves in 2 (M) x 2 (N); each wave owns a 128x128 block = 8x8 tiles of
-//    v_mfma_f32_16x16x32_bf16 (256 fp32 accumulators per lane, in the AGPR half of the unified
-//    register file).  Per 64-deep k-step a wave issues 128 MFMAs (2048 matrix-pipe cycles)
-//    against 32 fragment reads and 16 LDS-DMA pieces: a quarter of the LDS fragment bytes per
-//    FLOP of the 8-wave 128x64 tiling, and no partner wave competing for the SIMD's issue
-//    slots or its matrix pipe.
-//  * k advances in 64-deep steps through two 64 KiB LDS stages (A [256 rows][128 B] + B);
-//    each step is two half-steps of 64 MFMAs (k 0-31, k 32-63).  The fragments of the next
-//    half-step are read from LDS between this half-step's MFMAs (double-buffered in
-//    registers), so the matrix pipe never waits on a ds_read.
-//  * one barrier per step, between its two halves: every wave has retired its reads of the
-//    step's stage (lgkmcnt) and its DMAs of the next stage (vmcnt); after it the step's stage
-//    is refilled (stage s + 2) by LDS-DMA issued between the second half's MFMAs, while the
-//    second half reads the first fragments of stage s + 1.  Every DMA piece is 8 whole 128-B
-//    rows (k-major) or 4 whole 256-B k-rows (row-major-in-k), the full-line shape.
-//  * epilogues: the 8-wave kernel's finish256 (bias, quick_gelu + pre-activation store,
-//    residual, gelu' of the stored pre-activation) on each 128x64 half of the wave's block,
-//    bf16 rows staged through the then idle LDS stages so every store instruction writes
-//    whole 128-B rows.
+//    v_mfma_f32_16x16x32_bf16 (256 fp32 accumulators per lane, pinned in the AGPR half of the
+//    unified register file by inline-asm MFMAs).  Per 64-deep k-step a wave issues 128 MFMAs
+//    (2048 matrix-pipe cycles) against 32 fragment reads and 16 LDS-DMA pieces: half the LDS
+//    fragment bytes per FLOP of the 8-wave 128x64 tiling, and no partner wave competing for the
+//    SIMD's issue slots or its matrix pipe.
+//  * k advances in 64-deep steps through two 64 KiB LDS stages (A + B images); each step is two
+//    half-steps of 64 MFMAs.  The next half-step's fragments are read between this half-step's
+//    MFMAs (double-buffered in registers), so the matrix pipe never waits on a ds_read.
+//  * one barrier per step, between its two halves: every wave has retired its reads of the step's
+//    stage (lgkmcnt) and its DMAs of the next stage (vmcnt); after it the step's stage is refilled
+//    (stage s + 2) by LDS-DMA issued between the second half's MFMAs, while the second half reads
+//    the first fragments of stage s + 1.  Every DMA piece is 8 whole 128-B rows (k-major operand)
+//    or 4 whole 256-B k-rows (row-major-in-k operand, read back with ds_read_b64_tr_b16).
+//  * measured limit (tools/w4_stamps.py, profiles/r03_w4_*): the main loop runs at ~2.7-2.9k
+//    cycles per step against 2048 of MFMA work, bound by the CU's LDS-DMA issue rate (~24 B/clk:
+//    without the DMAs a step takes 2.37k cycles, without the fragment reads 2.87k); cache policy
+//    (nt / sc1) and fewer M0 writes do not move it.
+//  * persistent form (production): one workgroup per CU walks (split, tile) items; the next
+//    item's first two stages are DMA'd before this item's epilogue, which stages its rows in the
+//    32 KiB past the two stages, so the prologue latency (~6.7k cycles) hides under the stores.
+//  * epilogues: the 8-wave kernel's finish256 (bias, quick_gelu + pre-activation store, residual,
+//    gelu' of the stored pre-activation; fp32 beta / split-K slabs for weight gradients) on each
+//    128x64 half of the wave's block.  Weight gradients fuse the bias gradient as one extra MFMA
+//    per A fragment against a ones fragment (waves wn == 0 of n-tile 0), per-split partials summed
+//    in split order afterwards (deterministic).
 #include "gemm_common.h"
 
 namespace cmg {
@@ -44,68 +52,83 @@ int num_cus_w4() {
 }
 
 // Per-lane byte offsets, all 32-bit (a 256-row tile spans < 2 GiB).  Loop-invariant pieces are
-// computed once; the k-step varies only the stage base (LDS) and the descriptor base (DMA).
+// computed once; a k-step varies only the stage base (LDS) and the descriptor base (DMA).
+//   k-major operand ([rows][K]): image [256 rows][128 B], chunk c at c ^ ((r >> 1) & 7);
+//     fragment i at rd[kk] + i * 2048; DMA piece i at dma[i & 1] + (64 wave + 8 i) * ld * 2.
+//   row-major-in-k operand ([K][rows]): two [64 k][128] images of 16 KiB, chunk c at c ^ swz(k);
+//     fragment i at rd[kk] + ((i << 5) ^ sw); DMA piece i at dma[(i >> 1) & 1] + scalar part.
 struct W4Lane {
-  int a_rd[2];  // A fragment i of k-half kk at stage + a_rd[kk] + i * 2048
-  int b_rd[2];  // B: k-major as A; row-major-in-k: frag j at stage + b_rd[kk] + ((j << 5) ^ b_sw)
-  int b_sw;
-  int a_dma[2];  // A piece i: a_dma[i & 1] + (64 wave + 8 i) * lda * 2
-  int b_dma[2];  // B piece i: k-major as A; row-major-in-k b_dma[(i >> 1) & 1] + scalar
+  int a_rd[2], b_rd[2];
+  int a_sw, b_sw;
+  int a_dma[2], b_dma[2];
 };
 
-template <bool BKM>
-__device__ __forceinline__ W4Lane w4_lane(int wave, int lane, int64_t lda, int64_t ldb) {
-  W4Lane w;
-  const int wm = wave >> 1, wn = wave & 1;
+template <bool KMAJ>
+__device__ __forceinline__ void w4_lane_op(int base, int half, int lane, int64_t ld, int (&rd)[2], int& sw,
+                                           int (&dma)[2]) {
   const int l15 = lane & 15, l4 = lane >> 4;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    w.a_rd[kk] = (wm * 128 + l15) * 128 + (((kk * 4 + l4) ^ ((l15 >> 1) & 7)) << 4);
-    if (BKM) {
-      w.b_rd[kk] = 32768 + (wn * 128 + l15) * 128 + (((kk * 4 + l4) ^ ((l15 >> 1) & 7)) << 4);
+    if (KMAJ) {
+      rd[kk] = base + (half * 128 + l15) * 128 + (((kk * 4 + l4) ^ ((l15 >> 1) & 7)) << 4);
     } else {
       const int q = l15 >> 2, p4 = lane & 3;
-      w.b_rd[kk] = 32768 + wn * 16384 + (kk * 32 + 8 * l4 + q) * 256 + (p4 >> 1) * 16 + (p4 & 1) * 8;
+      rd[kk] = base + half * 16384 + (kk * 32 + 8 * l4 + q) * 256 + (p4 >> 1) * 16 + (p4 & 1) * 8;
     }
   }
-  w.b_sw = BKM ? 0 : (2 * (((l15 >> 2) & 3) | ((l4 & 1) << 2))) << 4;
+  sw = KMAJ ? 0 : (2 * (((l15 >> 2) & 3) | ((l4 & 1) << 2))) << 4;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    w.a_dma[p] = (lane >> 3) * (int)lda * 2 + (((lane & 7) ^ (4 * p + (lane >> 4))) << 4);
-    if (BKM) w.b_dma[p] = (lane >> 3) * (int)ldb * 2 + (((lane & 7) ^ (4 * p + (lane >> 4))) << 4);
-    else w.b_dma[p] = l4 * (int)ldb * 2 + (((lane & 15) ^ (2 * (l4 | (p << 2)))) << 4);
+    if (KMAJ) dma[p] = (lane >> 3) * (int)ld * 2 + (((lane & 7) ^ (4 * p + (lane >> 4))) << 4);
+    else dma[p] = l4 * (int)ld * 2 + (((lane & 15) ^ (2 * (l4 | (p << 2)))) << 4);
   }
+}
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ W4Lane w4_lane(int wave, int lane, int64_t lda, int64_t ldb) {
+  W4Lane w;
+  w4_lane_op<AK>(0, wave >> 1, lane, lda, w.a_rd, w.a_sw, w.a_dma);
+  w4_lane_op<BKM>(32768, wave & 1, lane, ldb, w.b_rd, w.b_sw, w.b_dma);
   return w;
 }
 
+#ifndef W4_CP  // cache-policy A/B builds of the main-loop DMAs (0 default, 1 nt, 2 sc1, 3 sc0 sc1)
+#define W4_CP 0
+#endif
+#if W4_CP == 1
+#define W4_DMA_POLICY " nt"
+#elif W4_CP == 2
+#define W4_DMA_POLICY " sc1"
+#elif W4_CP == 3
+#define W4_DMA_POLICY " sc0 sc1"
+#else
+#define W4_DMA_POLICY ""
+#endif
+
 // dma16 without its leading s_nop 2 (the wait states after the VALU readfirstlanes that wrote the
 // descriptor): inside the main loop the descriptor is built before the half-step's first four
-// MFMAs, so only the prologue's DMAs need the pad
+// MFMAs, so only the first piece after a fresh descriptor needs the pad (PAD)
+template <bool PAD>
 __device__ __forceinline__ void w4_dma(const SRsrc& r, char* lds, int voff) {
+  if (PAD) {
+    dma16(r, lds, voff);
+    return;
+  }
   const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, lds);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r.v)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" W4_DMA_POLICY " lds" ::"s"(m),
+               "v"(voff), "s"(r.v)
                : "memory");
 }
 
-template <bool PAD>
-__device__ __forceinline__ void w4_dmap(const SRsrc& r, char* lds, int voff) {
-  if (PAD) dma16(r, lds, voff);
-  else w4_dma(r, lds, voff);
-}
-
-// this wave's DMA piece i (0..7) of the A / B operand tile of one stage
-template <bool PAD = false>
-__device__ __forceinline__ void w4_piece_a(char* img, const SRsrc& rs, const W4Lane& w, int lda, int wave, int i) {
-  w4_dmap<PAD>(rs, img + (wave * 8 + i) * 1024, w.a_dma[i & 1] + (64 * wave + 8 * i) * lda * 2);
-}
-template <bool BKM, bool PAD = false>
-__device__ __forceinline__ void w4_piece_b(char* img, const SRsrc& rs, const W4Lane& w, int ldb, int wave, int i) {
-  if (BKM) {
-    w4_dmap<PAD>(rs, img + 32768 + (wave * 8 + i) * 1024, w.b_dma[i & 1] + (64 * wave + 8 * i) * ldb * 2);
+// this wave's DMA piece i (0..7) of one operand's 256x64 tile (image at img + base)
+template <bool KMAJ, bool PAD = false>
+__device__ __forceinline__ void w4_piece(char* img, int base, const SRsrc& rs, const int (&dma)[2], int ld, int wave,
+                                         int i) {
+  if (KMAJ) {
+    w4_dma<PAD>(rs, img + base + (wave * 8 + i) * 1024, dma[i & 1] + (64 * wave + 8 * i) * ld * 2);
   } else {
     const int jj = (wave & 1) * 8 + i;
-    w4_dmap<PAD>(rs, img + 32768 + (wave >> 1) * 16384 + jj * 1024,
-           w.b_dma[(i >> 1) & 1] + 4 * jj * ldb * 2 + (wave >> 1) * 256);
+    w4_dma<PAD>(rs, img + base + (wave >> 1) * 16384 + jj * 1024, dma[(i >> 1) & 1] + 4 * jj * ld * 2 + (wave >> 1) * 256);
   }
 }
 
@@ -117,64 +140,61 @@ __device__ __forceinline__ bf16x8 w4_rd_tr(const char* p) {
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 w4_frag(const char* p, int i, int sw) {
+  return KMAJ ? w4_rd(p + i * 2048) : w4_rd_tr(p + ((i << 5) ^ sw));
+}
 
 // acc += B-fragment x A-fragment (16x16x32 bf16).  Inline asm with an AGPR "+a" operand keeps
 // every accumulator in place in the AGPR file: with the builtin, the register allocator shuffles
 // the 256 accumulators between AGPRs and VGPRs across the loop's back edge (hundreds of
-// v_accvgpr moves per step).  Hazards the compiler does not see: accumulators are touched once
-// per half-step (64 MFMAs apart), operands come straight from ds_read, and the epilogue's first
-// AGPR read follows an explicit s_nop pad (w4_mfma_drain).
+// v_accvgpr moves per step) and spills.  Hazards the compiler does not see: accumulators are
+// touched once per half-step (64 MFMAs apart), operands come straight from ds_read, and the
+// epilogue's first AGPR read follows an explicit s_nop pad (w4_mfma_drain).
 __device__ __forceinline__ void w4_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
+// fused bias gradient: accb (VGPRs) += ones x A-fragment.  The leading s_nop 1 covers the
+// "VALU wrote an MFMA source VGPR" hazard in case the compiler re-materialises the ones operand
+// right before this (invisible-to-it) MFMA; the ones fragment is also laundered once per kernel
+// (w4_ones) so it lives in registers of its own.
+__device__ __forceinline__ void w4_mfma_v(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(b), "v"(a));
+}
+__device__ __forceinline__ bf16x8 w4_ones() {
+  bf16x8 o = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  asm volatile("" : "+v"(o));
+  return o;
+}
 __device__ __forceinline__ void w4_mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
 
-// One half-step: 64 MFMAs on the current fragments (fa, fb), in 16 groups of 4; after each
-// group's MFMAs one of the next half-step's 16 fragments is read from stage rst, k-half kk
-// (READ) and DM of this wave's 16 DMA pieces of the stage after next are issued into dimg (DMA).
-typedef __attribute__((ext_vector_type(16))) float w4f32x16;
-__device__ __forceinline__ void w4_mfma32(w4f32x16& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
-}
-
-template <bool BKM, bool READ, bool DMA, int DM, int DMODE = 0, bool M32 = false>
-__device__ __forceinline__ void w4_half(f32x4 (&acc)[2][8][4], w4f32x16 (&acc32)[16], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
-                                        bf16x8 (&na)[8], bf16x8 (&nb)[8], const char* rst, int kk, const W4Lane& w,
-                                        int wave, char* dimg, const SRsrc& ra, const SRsrc& rb, int lda, int ldb) {
+// One half-step: 64 MFMAs on the current fragments (fa, fb) in 16 groups of 4; after each group
+// one of the next half-step's 16 fragments is read from stage rst, k-half kk (READ) and one of
+// this wave's 16 DMA pieces of the stage after next is issued into dimg (DMA).  BG: 8 more MFMAs
+// summing the A fragments into the bias-gradient accumulators (waves that own bias rows).
+template <bool AK, bool BKM, bool READ, bool DMA, bool BG>
+__device__ __forceinline__ void w4_half(f32x4 (&acc)[2][8][4], f32x4 (&accb)[8], bool bias_wave, const bf16x8& ones,
+                                        const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], bf16x8 (&na)[8],
+                                        bf16x8 (&nb)[8], const char* rst, int kk, const W4Lane& w, int wave,
+                                        char* dimg, const SRsrc& ra, const SRsrc& rb, int lda, int ldb) {
   const char* pa = rst + w.a_rd[kk];
   const char* pb = rst + w.b_rd[kk];
-  int sw = w.b_sw;
-  asm volatile("" : "+v"(sw));  // keep the per-fragment swizzled addresses inside the loop
+  int swa = w.a_sw, swb = w.b_sw;
+  asm volatile("" : "+v"(swa), "+v"(swb));  // keep the per-fragment swizzled addresses inside the loop
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     const int i = g >> 1, h = g & 1;
-    if (M32) {  // timing experiment: 2 x 32x32x16 (64 cycles) in place of 4 x 16x16x32
-      w4_mfma32(acc32[(2 * g) & 15], fb[(2 * g) & 7], fa[i]);
-      w4_mfma32(acc32[(2 * g + 1) & 15], fb[(2 * g + 1) & 7], fa[i]);
-    } else {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) w4_mfma(acc[h][i][jj], fb[h * 4 + jj], fa[i]);
-    }
+    for (int jj = 0; jj < 4; ++jj) w4_mfma(acc[h][i][jj], fb[h * 4 + jj], fa[i]);
+    if (BG && h == 1 && bias_wave) w4_mfma_v(accb[i], ones, fa[i]);
     if (READ) {
-      if (g < 8) na[g] = w4_rd(pa + g * 2048);
-      else if (BKM) nb[g - 8] = w4_rd(pb + (g - 8) * 2048);
-      else nb[g - 8] = w4_rd_tr(pb + (((g - 8) << 5) ^ sw));
+      if (g < 8) na[g] = w4_frag<AK>(pa, g, swa);
+      else nb[g - 8] = w4_frag<BKM>(pb, g - 8, swb);
     }
-    if (DMA && DMODE == 1) {  // timing experiment: M0 written once per half-step (wrong LDS targets)
-      if (g == 0) {
-        const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, dimg);
-        asm volatile("s_nop 2\n\ts_mov_b32 m0, %0\n\ts_nop 0" ::"s"(m) : "memory");
-      }
-      const int voff = g < 8 ? w.a_dma[g & 1] + (64 * wave + 8 * g) * lda * 2 : w.b_dma[g & 1] + (64 * wave + 8 * (g - 8)) * ldb * 2;
-      asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"((g < 8 ? ra : rb).v) : "memory");
-    } else if (DMA) {
-#pragma unroll
-      for (int d = 0; d < DM; ++d) {
-        const int q = g * DM + d;
-        if (q == 0) w4_piece_a<true>(dimg, ra, w, lda, wave, q);
-        else if (q < 8) w4_piece_a(dimg, ra, w, lda, wave, q);
-        else if (q < 16) w4_piece_b<BKM>(dimg, rb, w, ldb, wave, q - 8);
-      }
+    if (DMA) {
+      if (g == 0) w4_piece<AK, true>(dimg, 0, ra, w.a_dma, lda, wave, 0);
+      else if (g < 8) w4_piece<AK>(dimg, 0, ra, w.a_dma, lda, wave, g);
+      else w4_piece<BKM>(dimg, 32768, rb, w.b_dma, ldb, wave, g - 8);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -198,17 +218,37 @@ __device__ __forceinline__ void w4_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// ST (diagnostic build, variant 22): s_memtime stamps into LDS past the two stages, copied to
-// p.dbg at the end: [0] kernel start, [1] main loop start, [2] main loop end, [3] kernel end,
-// [4 + 2s] / [5 + 2s] step s's barrier entry / exit (s < 58), [126] / [127] s_memrealtime at
-// kernel start / end (100 MHz).  Only lane 0 of each wave writes; the stamps' SMEM waits
-// perturb the schedule a little (cdna_hip_programming.md §7, in-kernel stamps).
+template <bool AK, bool BKM>
+__device__ __forceinline__ void w4_stage_dma(char* img, const GemmP& p, const W4Lane& w, int wave, int m0, int n0,
+                                             int k0, int kend, bool live) {
+  const SRsrc ra = w4_rsrc<AK>((const bf16*)p.A, p.lda, m0, p.M, k0, kend, live);
+  const SRsrc rb = w4_rsrc<BKM>((const bf16*)p.B, p.ldb, n0, p.N, k0, kend, live);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w4_piece<AK, true>(img, 0, ra, w.a_dma, (int)p.lda, wave, i);
+    w4_piece<BKM, true>(img, 32768, rb, w.b_dma, (int)p.ldb, wave, i);
+  }
+}
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void w4_first_frags(const char* smem, const W4Lane& w, bf16x8 (&a0)[8], bf16x8 (&b0)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = w4_frag<AK>(smem + w.a_rd[0], i, w.a_sw);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = w4_frag<BKM>(smem + w.b_rd[0], j, w.b_sw);
+}
+
+// ------------------------------------------------------------------ one tile per workgroup
+// The first form, kept for its diagnostic builds (ST: s_memtime stamps into LDS past the two
+// stages, copied to p.dbg: [0] kernel start, [1] main loop start, [2] main loop end, [3] kernel
+// end, [4 + 2s] / [5 + 2s] step s's barrier entry / exit (s < 58), [126] / [127] s_memrealtime at
+// kernel start / end; NOLD bit 0: no main-loop DMAs, bit 1: no fragment reads -- timing only).
 constexpr int W4_NST = 128;
 __device__ __forceinline__ void w4_stamp(char* smem, int wave, int lane, int k, unsigned long long v) {
   if (lane == 0) *LDS_PTR(unsigned long long, smem + 2 * W4_STAGE + (wave * W4_NST + k) * 8) = v;
 }
 
-template <bool BKM, typename OutT, int EPI, int DM, bool ST = false, int NOLD = 0>
+template <bool BKM, typename OutT, int EPI, bool ST = false, int NOLD = 0>
 __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
@@ -225,10 +265,8 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
   const int m0 = tm * BT, n0 = tn * BT;
   const int K = p.K;
   const int ns = (K + 63) / 64;
-  const bf16* A = (const bf16*)p.A;
-  const bf16* B = (const bf16*)p.B;
+  const W4Lane w = w4_lane<true, BKM>(wave, lane, p.lda, p.ldb);
   const int lda = (int)p.lda, ldb = (int)p.ldb;
-  const W4Lane w = w4_lane<BKM>(wave, lane, p.lda, p.ldb);
 
   f32x4 acc[2][8][4];
 #pragma unroll
@@ -237,74 +275,47 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
-  w4f32x16 acc32[16];  // timing experiment only (NOLD & 8)
-  if (NOLD & 8) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc32[i] = w4f32x16{};
-  }
 
   // prologue: stages 0 and 1 in flight, stage 0 waited for, first fragments read
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (s < ns) {
-      char* img = smem + s * W4_STAGE;
-      const SRsrc ra = srsrc256<true>(A, p.lda, m0, p.M, s * 64, K);
-      const SRsrc rb = srsrc256<BKM>(B, p.ldb, n0, p.N, s * 64, K);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        w4_piece_a<true>(img, ra, w, lda, wave, i);
-        w4_piece_b<BKM, true>(img, rb, w, ldb, wave, i);
-      }
-    }
-  }
+  if (ns > 0) w4_stage_dma<true, BKM>(smem, p, w, wave, m0, n0, 0, K, true);
+  if (ns > 1) w4_stage_dma<true, BKM>(smem + W4_STAGE, p, w, wave, m0, n0, 64, K, true);
   __builtin_amdgcn_sched_barrier(0);
   if (ns > 1) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if (ns > 0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a0[i] = w4_rd(smem + w.a_rd[0] + i * 2048);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b0[j] = BKM ? w4_rd(smem + w.b_rd[0] + j * 2048) : w4_rd_tr(smem + w.b_rd[0] + ((j << 5) ^ w.b_sw));
-  }
+  if (ns > 0) w4_first_frags<true, BKM>(smem, w, a0, b0);
 
   // One loop body for every step (a single code path keeps the 256 accumulators in place):
   // past the last stage the DMAs get an empty descriptor (the hardware's range check turns them
   // into zero writes of a stage nobody reads) and the reads fetch fragments nobody uses.
   unsigned long long st_loop = 0, st_a = 0, st_b = 0;
   if (ST) st_loop = __builtin_amdgcn_s_memtime();
+  const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
   for (int s = 0; s < ns; ++s) {
     char* img = smem + (s & 1) * W4_STAGE;
     char* nxt = smem + ((s + 1) & 1) * W4_STAGE;
-    const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
-    // half 0: k 0-31 of stage s; read k 32-63 of stage s
-    w4_half<BKM, !(NOLD & 2), false, DM, 0, (NOLD & 8) != 0>(acc, acc32, a0, b0, a1, b1, img, 1, w, wave, nullptr,
-                                                           none, none, 0, 0);
-    // stage s retired by every wave's reads, stage s + 1 landed
+    w4_half<true, BKM, !(NOLD & 2), false, false>(acc, accb, false, a0[0], a0, b0, a1, b1, img, 1, w, wave, nullptr, none,
+                                                  none, 0, 0);
     if (ST) st_a = __builtin_amdgcn_s_memtime();
     w4_sync();
     if (ST) st_b = __builtin_amdgcn_s_memtime();
-    // half 1: k 32-63 of stage s; read k 0-31 of stage s + 1; refill this stage with s + 2
     const bool more = s + 2 < ns;
-    const SRsrc ra = w4_rsrc<true>(A, p.lda, m0, p.M, (s + 2) * 64, K, more);
-    const SRsrc rb = w4_rsrc<BKM>(B, p.ldb, n0, p.N, (s + 2) * 64, K, more);
-    w4_half<BKM, !(NOLD & 2), !(NOLD & 1), DM, (NOLD & 4) ? 1 : 0, (NOLD & 8) != 0>(acc, acc32, a1, b1, a0, b0, nxt, 0,
-                                                                                  w, wave, img, ra, rb, lda, ldb);
+    const SRsrc ra = w4_rsrc<true>((const bf16*)p.A, p.lda, m0, p.M, (s + 2) * 64, K, more);
+    const SRsrc rb = w4_rsrc<BKM>((const bf16*)p.B, p.ldb, n0, p.N, (s + 2) * 64, K, more);
+    w4_half<true, BKM, !(NOLD & 2), !(NOLD & 1), false>(acc, accb, false, a1[0], a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb,
+                                                        lda, ldb);
     if (ST && s < 58) {
       w4_stamp(smem, wave, lane, 4 + 2 * s, st_a);
       w4_stamp(smem, wave, lane, 5 + 2 * s, st_b);
     }
   }
-  // every wave passed the last step's barrier after its last LDS read and DMA: the stages are
-  // idle, so the epilogue may stage rows in this wave's 16 KiB of them
   w4_mfma_drain();
-  if (NOLD & 8) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) asm volatile("" ::"a"(acc32[i]));
-  }
   unsigned long long st_lend = 0;
   if (ST) st_lend = __builtin_amdgcn_s_memtime();
+  // every wave passed the last step's barrier after its last useful LDS read and DMA: the stages
+  // are idle, so the epilogue may stage rows in this wave's 16 KiB of them
   char* st = smem + wave * 16384;
   finish256<OutT, EPI, true>(p, acc[0], m0 + wm * 128, n0 + wn * 128, lane, 0, st);
   finish256<OutT, EPI, true>(p, acc[1], m0 + wm * 128, n0 + wn * 128 + 64, lane, 0, st);
@@ -327,132 +338,139 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
   }
 }
 
-
-// Persistent form: one workgroup per CU walks tiles blockIdx' , blockIdx' + grid, ... (the same
-// XCD-aware order as the one-tile kernel, round by round).  After a tile's main loop the next
-// tile's first two stages are DMA'd into the (now idle) stage buffers BEFORE this tile's
-// epilogue runs, so the next tile's prologue latency (~6.7k cycles per tile measured with
-// tools/w4_stamps.py) hides behind the epilogue's stores; the epilogue stages its rows in the
-// 32 KiB past the two stages (8 KiB per wave).  p.stagger > 0: half the workgroups of every XCD
-// start p.stagger x s_sleep(127) later, desynchronising the CUs' epilogue store bursts.
-template <bool BKM, typename OutT, int EPI>
-__global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p) {
+// ------------------------------------------------------------------ persistent (production)
+// One workgroup per CU walks items i = r * grid + xcd_remap(blockIdx) (item = split * ntiles +
+// tile, so each XCD holds a contiguous run of one k-slab's tiles per round).  After an item's
+// main loop the next item's first two stages are DMA'd into the (now idle) stage buffers BEFORE
+// this item's epilogue runs, so the next prologue's latency hides behind the epilogue's stores;
+// the epilogue stages its rows in the 32 KiB past the two stages (8 KiB per wave).  p.stagger > 0:
+// half the workgroups of every XCD start p.stagger x s_sleep(127) later (A/B of desynchronised
+// epilogue bursts: measured neutral).
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+__global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nwg = gridDim.x;
-  int tile = xcd_remap(blockIdx.x, nwg);
-  if (tile >= p.ntiles) return;
-  const int K = p.K;
-  const int ns = (K + 63) / 64;
-  const bf16* A = (const bf16*)p.A;
-  const bf16* B = (const bf16*)p.B;
+  const int splits = (p.K + p.k_per_split - 1) / p.k_per_split;
+  const int nitems = p.ntiles * max(1, splits);
+  int item = xcd_remap(blockIdx.x, nwg);
+  if (item >= nitems) return;
   const int lda = (int)p.lda, ldb = (int)p.ldb;
-  const W4Lane w = w4_lane<BKM>(wave, lane, p.lda, p.ldb);
+  const W4Lane w = w4_lane<AK, BKM>(wave, lane, p.lda, p.ldb);
   if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   }
-  auto prologue_dma = [&](int tl) {  // stages 0 and 1 of tile tl
+  auto coords = [&](int it, int& m0, int& n0, int& kz, int& kbeg, int& kend) {
+    kz = it / p.ntiles;
     int tm, tn;
-    tile_coords(p, tl, tm, tn);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      char* img = smem + s * W4_STAGE;
-      const SRsrc ra = w4_rsrc<true>(A, p.lda, tm * BT, p.M, s * 64, K, s < ns);
-      const SRsrc rb = w4_rsrc<BKM>(B, p.ldb, tn * BT, p.N, s * 64, K, s < ns);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        w4_piece_a<true>(img, ra, w, lda, wave, i);
-        w4_piece_b<BKM, true>(img, rb, w, ldb, wave, i);
-      }
-    }
+    tile_coords(p, it - kz * p.ntiles, tm, tn);
+    m0 = tm * BT;
+    n0 = tn * BT;
+    kbeg = kz * p.k_per_split;
+    kend = min(p.K, kbeg + p.k_per_split);
   };
-  prologue_dma(tile);
+  auto prologue_dma = [&](int it) {  // stages 0 and 1 of item it
+    int m0, n0, kz, kbeg, kend;
+    coords(it, m0, n0, kz, kbeg, kend);
+    const int ns = (kend - kbeg + 63) / 64;
+    w4_stage_dma<AK, BKM>(smem, p, w, wave, m0, n0, kbeg, kend, ns > 0);
+    w4_stage_dma<AK, BKM>(smem + W4_STAGE, p, w, wave, m0, n0, kbeg + 64, kend, ns > 1);
+  };
+  prologue_dma(item);
   f32x4 acc[2][8][4];
+  f32x4 accb[8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
-  w4f32x16 acc32[16];  // unused (w4_half's timing-experiment operand)
+  const bf16x8 ones = w4_ones();
   const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
   while (true) {
-    int tm, tn;
-    tile_coords(p, tile, tm, tn);
-    const int m0 = tm * BT, n0 = tn * BT;
+    int m0, n0, kz, kbeg, kend;
+    coords(item, m0, n0, kz, kbeg, kend);
+    const int ns = (kend - kbeg + 63) / 64;
+    const bool bias_wave = BG && n0 == 0 && wn == 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // this tile's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed
+    if (BG) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // this item's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed
     w4_sync();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a0[i] = w4_rd(smem + w.a_rd[0] + i * 2048);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b0[j] = BKM ? w4_rd(smem + w.b_rd[0] + j * 2048) : w4_rd_tr(smem + w.b_rd[0] + ((j << 5) ^ w.b_sw));
+    w4_first_frags<AK, BKM>(smem, w, a0, b0);
     for (int s = 0; s < ns; ++s) {
       char* img = smem + (s & 1) * W4_STAGE;
       char* nxt = smem + ((s + 1) & 1) * W4_STAGE;
-      w4_half<BKM, true, false, 1>(acc, acc32, a0, b0, a1, b1, img, 1, w, wave, nullptr, none, none, 0, 0);
+      w4_half<AK, BKM, true, false, BG>(acc, accb, bias_wave, ones, a0, b0, a1, b1, img, 1, w, wave, nullptr, none, none, 0,
+                                        0);
       w4_sync();
       const bool more = s + 2 < ns;
-      const SRsrc ra = w4_rsrc<true>(A, p.lda, m0, p.M, (s + 2) * 64, K, more);
-      const SRsrc rb = w4_rsrc<BKM>(B, p.ldb, n0, p.N, (s + 2) * 64, K, more);
-      w4_half<BKM, true, true, 1>(acc, acc32, a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb, lda, ldb);
+      const SRsrc ra = w4_rsrc<AK>((const bf16*)p.A, p.lda, m0, p.M, kbeg + (s + 2) * 64, kend, more);
+      const SRsrc rb = w4_rsrc<BKM>((const bf16*)p.B, p.ldb, n0, p.N, kbeg + (s + 2) * 64, kend, more);
+      w4_half<AK, BKM, true, true, BG>(acc, accb, bias_wave, ones, a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb, lda, ldb);
     }
     w4_mfma_drain();
-    const int next = tile + nwg;
-    // every wave's last useful stage read came before the last step's barrier (the final half-step's
-    // reads fetch fragments nobody uses), so the next tile's prologue may overwrite both stages
-    if (next < p.ntiles) prologue_dma(next);
+    const int next = item + nwg;
+    // every wave's last useful stage read came before the last step's barrier (the final
+    // half-step's reads fetch fragments nobody uses), so the next item may overwrite both stages
+    if (next < nitems) prologue_dma(next);
+    if (BG && bias_wave && lane < 16) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + lane;
+        if (m < p.M) {
+          if (p.bws) p.bws[(int64_t)kz * p.M + m] = accb[i][0];  // summed in split order afterwards
+          else atomicAdd(bias_grad + m, accb[i][0]);             // one split: one add per element
+        }
+      }
+    }
     char* st = smem + 2 * W4_STAGE + wave * 8192;
-    finish256<OutT, EPI, true>(p, acc[0], m0 + wm * 128, n0 + wn * 128, lane, 0, st);
-    finish256<OutT, EPI, true>(p, acc[1], m0 + wm * 128, n0 + wn * 128 + 64, lane, 0, st);
-    if (next >= p.ntiles) break;
-    tile = next;
+    finish256<OutT, EPI, true>(p, acc[0], m0 + wm * 128, n0 + wn * 128, lane, kz, st);
+    finish256<OutT, EPI, true>(p, acc[1], m0 + wm * 128, n0 + wn * 128 + 64, lane, kz, st);
+    if (next >= nitems) break;
+    item = next;
   }
 }
 
-template <bool BKM, int EPI>
-void launch_w4p(const GemmP& p, hipStream_t s) {
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
-  (void)lds_optin((const void*)gemm_w4p_kernel<BKM, bf16, EPI>, L);
-  const int grid = std::min(p.ntiles, num_cus_w4());
-  hipLaunchKernelGGL((gemm_w4p_kernel<BKM, bf16, EPI>), dim3(grid), dim3(W4_THR), L, s, p);
+  (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>, L);
+  const int grid = std::min(p.ntiles * splits, num_cus_w4());
+  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
 }
 
 template <bool BKM, int EPI>
 void launch_w4(const GemmP& p, hipStream_t s, int dm) {
   if (dm == 100) {
-    launch_w4p<BKM, EPI>(p, s);
+    launch_w4p<true, BKM, bf16, EPI, false>(p, 1, s, nullptr);
     return;
   }
-  if (dm < 0) {
+  if (dm < 0) {  // diagnostic stamp builds
     constexpr int L = 2 * W4_STAGE + 4 * W4_NST * 8;
 #define W4_ST(n)                                                                                              \
-  (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI, 1, true, n>, L);                               \
-  hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI, 1, true, n>), dim3(p.ntiles), dim3(W4_THR), L, s, p)
+  (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI, true, n>, L);                                  \
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI, true, n>), dim3(p.ntiles), dim3(W4_THR), L, s, p)
     if (dm == -1) { W4_ST(0); }
     else if (dm == -2) { W4_ST(1); }
     else if (dm == -3) { W4_ST(2); }
-    else if (dm == -4) { W4_ST(3); }
-    else if (dm == -5) { W4_ST(4); }
-    else { W4_ST(8); }
+    else { W4_ST(3); }
 #undef W4_ST
     return;
   }
-  if (dm == 2) {
-    (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI, 2>, 2 * W4_STAGE);
-    hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI, 2>), dim3(p.ntiles), dim3(W4_THR), 2 * W4_STAGE, s, p);
-  } else {
-    (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI, 1>, 2 * W4_STAGE);
-    hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI, 1>), dim3(p.ntiles), dim3(W4_THR), 2 * W4_STAGE, s, p);
-  }
+  (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI>, 2 * W4_STAGE);
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI>), dim3(p.ntiles), dim3(W4_THR), 2 * W4_STAGE, s, p);
 }
 
 }  // namespace
 
 // forward (k-major B) and dgrad (row-major-in-k B) products with bf16 output and one of the
 // CLIP path's epilogues; returns the profiler label, or nullptr when not covered.
+// dm: 1 one tile per workgroup, 100 persistent, < 0 the stamped diagnostic builds.
 const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int dm) {
   constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU;
   constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU;
@@ -471,6 +489,20 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
     case E_DQ: launch_w4<false, E_DQ>(p, s, dm); return "gemm256_dgrad_dqgelu";
     default: return nullptr;
   }
+}
+
+// weight gradients (both operands row-major in k, fp32 output): split-K slabs (p.ws) or the
+// beta epilogue (one split), with the fused bias gradient when bg != nullptr
+const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg) {
+  if (p.ws) {
+    if (bg) launch_w4p<false, false, float, 0, true>(p, splits, s, bg);
+    else launch_w4p<false, false, float, 0, false>(p, splits, s, bg);
+    return "gemm256_wgrad_splitk";
+  }
+  if (flags != CLIPMI_EPI_BETA) return nullptr;
+  if (bg) launch_w4p<false, false, float, CLIPMI_EPI_BETA, true>(p, 1, s, bg);
+  else launch_w4p<false, false, float, CLIPMI_EPI_BETA, false>(p, 1, s, bg);
+  return "gemm256_wgrad";
 }
 
 }  // namespace cmg

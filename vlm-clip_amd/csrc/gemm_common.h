@@ -585,5 +585,7 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
 
 // 4-wave 256x256 kernel (gemm4.hip) for the forward / dgrad layouts; nullptr if not covered
 const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int dm);
+// its persistent weight-gradient form (both operands row-major in k, fp32 out, split-K slabs)
+const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg);
 
 }  // namespace cmg
