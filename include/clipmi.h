@@ -9,6 +9,14 @@
  *
  * The reference has no native boundary: its hot path is PyTorch/HF
  * module calls.  Each entry point below names the reference op it replaces.
+ *
+ * Collectives are not in this ABI.  SURVEY.md §8b sketched clipmi_ctx / clipmi_workspace_size /
+ * clipmi_allgather_embed / clipmi_reducescatter_grad / clipmi_allreduce_grads; the build keeps the
+ * host side PyTorch-ROCm as north_star allows, so the data-parallel exchanges (all-gather of the
+ * normalised features, reduce-scatter of their gradients, the bucketed gradient all-reduce) are
+ * issued through torch.distributed (backend "nccl" = RCCL over xGMI) by clipmi/towers.py
+ * (ContrastiveFn) and clipmi/trainer.py (GradBucketReducer), on the same HIP streams these entry
+ * points run on.  Workspaces are sized per call by the *_ws() queries (no context object).
  */
 #ifndef CLIPMI_H
 #define CLIPMI_H
@@ -26,6 +34,8 @@ enum clipmi_dtype { CLIPMI_F32 = 0, CLIPMI_BF16 = 1, CLIPMI_FP8 = 2 /* MXFP8: OC
 
 int clipmi_version(void);
 const char* clipmi_last_error(void);
+/* sha256 (hex) of the sources this library was compiled from (vlm-clip_amd/Makefile DIGEST_SRC) */
+const char* clipmi_build_digest(void);
 
 /* ---- GEMM:  C[m,n] = epi( alpha * sum_k A(m,k) B(n,k) )  --------------------------
  * Replaces nn.Linear forward/backward inside HF CLIPAttention/CLIPMLP
@@ -58,7 +68,7 @@ typedef struct clipmi_gemm_desc {
   int force_small_tile; /* 1: 128x128 register-staged kernel; >=2: 256-kernel schedule variant (bench) */
   /* ab_dtype == CLIPMI_FP8 (BASELINE config 5, forward GEMMs of the frozen towers): A, B are OCP e4m3
    * bytes, both k-major, K % 128 == 0; a_scale / b_scale are E8M0 bytes [rows][K/32] (OCP MX:
-   * element value = fp8 * 2^(scale - 127)); v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation,
+   * element value = fp8 * 2^(scale - 127)); v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation,
    * the bf16 epilogues.  c_dtype == CLIPMI_FP8 (flags bias and/or quick_gelu / gelu only, ldc == N,
    * N % 32 == 0): C is written as MXFP8 too, e4m3 bytes [M, N] and E8M0 scales c_scale [M, N/32]
    * (fc1 -> fc2 without a bf16 round trip). */
@@ -126,8 +136,8 @@ int clipmi_text_embed_bwd(void* stream, int dtype, const int64_t* ids, const voi
 int clipmi_im2col(void* stream, int dtype, const float* pixels, void* X, int B, int C, int H, int P, int Kp);
 /* The input step (CLIPImageProcessor's center_crop + rescale + normalize, [HF]
  * image_processing_clip.py) fused into the same im2col: uint8 images [B, Hin, Win, 3]
- * (channels last), centre-cropped to image_size, (u/255 - mean[c]) / std[c].  Resizing
- * stays on the host.  P even (16/32: 8 pixels per thread; ViT-L/14: 2), Kp == 3*P*P or padded
+ * (channels last), centre-cropped to image_size, (u/255 - mean[c]) / std[c].  The shortest-edge
+ * resize before it is clipmi_resize_u8 below.  P even (16/32: 8 pixels per thread; ViT-L/14: 2), Kp == 3*P*P or padded
  * to a multiple of 8 (the pad columns are zeroed: L/14's 588 -> 640); mean/std are 3 host floats. */
 int clipmi_im2col_u8(void* stream, int dtype, const uint8_t* images, void* X, int B, int Hin, int Win, int image_size,
                      int P, int Kp, const float* mean, const float* std);
@@ -144,7 +154,8 @@ int clipmi_gather_rows(void* stream, int dtype, const void* src, const int* idx,
 int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx, int B, int S, int D, void* dst,
                         int beta);
 
-/* ---- Attention (head_dim 64, N <= 288) ([HF] CLIPAttention :298-335, eager core :259-277) -----
+/* ---- Attention (head_dim 64, N <= 4096: K/V resident in LDS up to N = 288, K/V streamed above;
+ * [HF] CLIPAttention :298-335, eager core :259-277) -----
  * qkv: [B*N, 3D] (q | k | v, head h at h*64), o: [B*N, D], lse: [B*H*N] fp32.
  * attention_mask: int64 [B, N] key padding (1 keep) or NULL; causal for the text tower. */
 int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse, const int64_t* attention_mask,

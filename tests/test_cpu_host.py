@@ -32,6 +32,14 @@ def test_library_exports_every_declared_symbol():
     assert L.clipmi_version() >= 1
 
 
+def test_library_built_from_these_sources():
+    """Build provenance: the loaded libclipmi.so carries the sha256 of the sources it was compiled
+    from (Makefile DIGEST_SRC), equal to the digest of the sources in this tree -- the same check
+    _lib.lib() makes before any op runs, here or on a GPU box."""
+    from clipmi import _lib
+    assert _lib.build_digest() == _lib.source_digest()
+
+
 def test_invalid_args_raise_without_gpu():
     """Argument validation runs on the host before any launch."""
     from clipmi import _lib

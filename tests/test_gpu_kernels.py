@@ -270,7 +270,10 @@ def test_contrastive_fn_matches_torch(B, E):
     assert abs(ar.grad[0].item() - lr_.grad.item()) < 1e-4 * max(1, abs(lr_.grad.item()))
 
 
-@pytest.mark.parametrize("B,E,chunk", [(1000, 512, 256), (1000, 512, 333), (4096, 768, 1024), (64, 64, 1)])
+@pytest.mark.parametrize("B,E,chunk", [(1000, 512, 256), (1000, 512, 333), (4096, 768, 1024), (64, 64, 1),
+                                        # config 5's global batch on one GPU: Bg = 32768 columns in
+                                        # [32768, 8192] chunks vs the materialised 4.3 GB logits
+                                        (32768, 768, 8192)])
 def test_contrastive_streamed_matches_materialised(B, E, chunk, monkeypatch):
     """Column-streamed InfoNCE (Bg > CLIPMI_CE_CHUNK: online log-sum-exp over column chunks,
     chunk recompute in backward, [B, Bg] never materialised) against the plain path."""

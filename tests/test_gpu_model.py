@@ -448,7 +448,9 @@ def test_shared_adapters_training_dropout_matches_oracle_with_same_masks():
 # mantissa bits, one power-of-two scale per 32 inputs), i.e. ~2-3 % per element, over 24 + 12
 # layers; the logits (100 x cosine) are bounded by FP8_LOGIT_TOL and the features' direction by a
 # cosine similarity with the reference's.
-FP8_LOGIT_TOL = 2.0
+# Bounds ~2x the measured error (L/14@336 B=2: 0.23-0.28; B/32 B=8: 0.82 -- its 512-wide
+# features and 12-layer towers round more per logit than L/14's 768-wide ones).
+FP8_LOGIT_TOL = {"l14_336": 0.5, "b32": 1.6}
 FP8_FEATURE_COS = 0.99
 
 
@@ -470,8 +472,45 @@ def test_fp8_towers_match_reference(golden, tag, preset, B):
     ci = cos(out["image_features"].cpu().numpy(), g["image_features"])
     ct = cos(out["text_features"].cpu().numpy(), g["text_features"])
     print(f"\n[{tag} fp8] max|dlogit| {err:.4f} (bf16 {err16:.4f}); min feature cosine image {ci:.5f} text {ct:.5f}")
-    assert err < FP8_LOGIT_TOL, err
+    assert err < FP8_LOGIT_TOL[tag], err
     assert ci > FP8_FEATURE_COS and ct > FP8_FEATURE_COS, (ci, ct)
+
+
+# Per-depth fp8 error growth at L/14@336: the same synthetic weights truncated to the first d
+# layers of both towers (weights are drawn per parameter name, so depth d is a prefix of the full
+# model), fp8 features against this library's fp32 parity path (itself pinned to the reference by
+# forward_l14_336.npz at 1e-5).  Minimum per-sample feature cosine at every depth >= 0.99.
+FP8_DEPTH_COS = 0.99
+
+
+def test_fp8_feature_cosine_per_depth():
+    import dataclasses
+    base = C.resolve("L/14@336")
+    B = 2
+    rows = []
+    for d in (1, 2, 6, 12, 24):
+        cfg = dataclasses.replace(
+            base, name=f"l14_336_depth{d}",
+            vision_config=dataclasses.replace(base.vision_config, num_hidden_layers=d),
+            text_config=dataclasses.replace(base.text_config, num_hidden_layers=min(d, base.text_config.num_hidden_layers)))
+        feats = {}
+        for prec in ("fp32", "fp8"):
+            m = CLIPWithAdapters(cfg, use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                                 freeze_clip=True, device="cuda", precision=prec)
+            with torch.no_grad():
+                out = m(**batch(m.config, B))
+            feats[prec] = (out["image_features"].double(), out["text_features"].double())
+            del m, out
+        torch.cuda.empty_cache()
+
+        def cos(a, b):
+            return float(torch.nn.functional.cosine_similarity(a, b, dim=-1).min())
+        ci = cos(feats["fp8"][0], feats["fp32"][0])
+        ct = cos(feats["fp8"][1], feats["fp32"][1])
+        rows.append((d, ci, ct))
+        print(f"\n[fp8 depth {d:2d}] min feature cosine vs fp32: image {ci:.5f} text {ct:.5f}")
+    for d, ci, ct in rows:
+        assert ci > FP8_DEPTH_COS and ct > FP8_DEPTH_COS, (d, ci, ct)
 
 
 def test_fp8_rejects_training_towers():

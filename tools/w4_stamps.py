@@ -18,7 +18,11 @@ SH = {"fc1_fwd": (R, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_
       "fc2_fwd": (R, 768, 3072, True, _lib.EPI_BIAS | _lib.EPI_RESID),
       "qkv_fwd": (R, 2304, 768, True, _lib.EPI_BIAS), "out_fwd": (R, 768, 768, True, _lib.EPI_BIAS | _lib.EPI_RESID),
       "fc2_dgrad": (R, 3072, 768, False, _lib.EPI_DQGELU), "fc1_dgrad": (R, 768, 3072, False, 0),
-      "sq8k": (8192, 8192, 8192, True, 0)}
+      "sq8k": (8192, 8192, 8192, True, 0),
+      # few-tile shapes (~60 workgroups = ~60 storing CUs): the epilogue's per-CU rate when the chip's
+      # write bandwidth is not shared by all 256 CUs
+      "qkv_fwd_60": (7 * 256, 2304, 768, True, _lib.EPI_BIAS),
+      "fc1_fwd_60": (5 * 256, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE)}
 _lib.declare("clipmi_gemm_stamps", [ctypes.c_void_p])
 L = _lib.lib()
 buf = torch.zeros(512 * 4 * 128, dtype=torch.int64, device="cuda")
@@ -34,7 +38,10 @@ for name in sys.argv[1:] or ["fc1_dgrad"]:
     f = lambda v: K.gemm(M, N, Kd, A, Kd, True, B, Kd if bkm else N, bkm, C, N, small_tile=v, **kw)
     for _ in range(3):
         f(20)
-    for var, what in ((22, "production"), (23, "no main-loop DMAs"), (24, "no fragment reads"), (25, "MFMAs only")):
+    vs = ((22, "production"), (23, "no main-loop DMAs"), (24, "no fragment reads"), (25, "MFMAs only"))
+    if os.environ.get("W4_ST_PROD_ONLY"):
+        vs = vs[:1]
+    for var, what in vs:
         L.clipmi_gemm_stamps(ctypes.c_void_p(buf.data_ptr()))
         f(var)
         torch.cuda.synchronize()

@@ -49,6 +49,7 @@ def _declare(name, restype, argtypes):
 
 
 _declare("clipmi_version", ctypes.c_int, [])
+_declare("clipmi_build_digest", ctypes.c_char_p, [])
 _declare("clipmi_last_error", ctypes.c_char_p, [])
 _declare("clipmi_gemm", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc)])
 
@@ -61,6 +62,26 @@ def declare(name, argtypes, restype=ctypes.c_int):
         f.restype, f.argtypes = restype, argtypes
 
 
+def source_digest() -> str:
+    """sha256 of the library's sources as the Makefile computes it (sorted csrc/*.hip, *.cpp,
+    *.h, then include/clipmi.h), from the tree this package sits in."""
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    csrc = os.path.join(pkg, "csrc")
+    names = sorted(f"csrc/{n}" for n in os.listdir(csrc) if n.endswith((".hip", ".cpp", ".h")))
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(pkg, n), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(os.path.dirname(pkg), "include", "clipmi.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def build_digest() -> str:
+    return lib().clipmi_build_digest().decode()
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -71,6 +92,13 @@ def lib():
         for name, (res, args) in _PROTOS.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
+        # provenance: the library must be built from the sources next to it (an alternative
+        # CLIPMI_LIB build is an A/B experiment of other sources, so it is exempt)
+        if not os.environ.get("CLIPMI_LIB") and not os.environ.get("CLIPMI_ALLOW_STALE"):
+            built, src = L.clipmi_build_digest().decode(), source_digest()
+            if built != src:
+                raise ImportError(f"{LIB_PATH} was built from other sources (digest {built[:12]}, tree "
+                                  f"{src[:12]}); rebuild with `make -C vlm-clip_amd`")
         _lib = L
     return _lib
 

@@ -19,5 +19,10 @@ int clipmi_invalid(const std::string& msg) {
   return CLIPMI_ERR_INVALID;
 }
 
+#ifndef CLIPMI_SRC_DIGEST
+#define CLIPMI_SRC_DIGEST "unknown"
+#endif
+
 extern "C" int clipmi_version(void) { return 1; }
+extern "C" const char* clipmi_build_digest(void) { return CLIPMI_SRC_DIGEST; }
 extern "C" const char* clipmi_last_error(void) { return g_last_error.c_str(); }
