@@ -86,7 +86,8 @@ def synthetic_batch(cfg, B, rank, device, seed=1234):
 # Kernel families timed live (labels returned by libclipmi's dispatch, csrc/gemm.hip, attention.hip)
 FAMILIES = {
     "gemm256_fwd_dgrad": ["gemm256_fwd_bias", "gemm256_fwd_bias_resid", "gemm256_fwd_bias_qgelu_pre",
-                          "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad", "gemm256_dgrad_dqgelu"],
+                          "gemm256_fwd_bias_qgelu_dact", "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad",
+                          "gemm256_dgrad_dqgelu", "gemm256_dgrad_mulaux"],
     "gemm256_wgrad": ["gemm256_wgrad_splitk", "gemm256_wgrad"],
     "attention": ["attn_fwd", "attn_bwd"],
     "gemm_fp8": ["gemm_fp8_fwd_bias", "gemm_fp8_fwd_bias_resid", "gemm_fp8_fwd_bias_qgelu",

@@ -45,6 +45,7 @@ const char* clipmi_build_digest(void);
  * flags: bit0 bias[n] | bit1 quick_gelu | bit2 gelu_erf | bit3 += residual[m,n]
  *        bit4 *= quick_gelu'(aux[m,n]) | bit5 *= gelu_erf'(aux[m,n])
  *        bit6 C += result (beta = 1) | bit7 store pre-activation to aux[m,n]
+ *        bit8 store act'(pre-activation) to aux[m,n] | bit9 *= aux[m,n]
  * dtypes: A/B bf16 (MFMA path) or f32 (exact-f32 parity path); C/residual/aux in c_dtype.
  * split_k > 1 (fp32 C, beta flag only) uses workspace of split_k*M*N floats (+ split_k*M with
  * bias_grad: per-split bias partials summed in split order, so results are run-to-run identical).
@@ -85,6 +86,12 @@ typedef struct clipmi_gemm_desc {
 #define CLIPMI_EPI_DGELU 32
 #define CLIPMI_EPI_BETA 64
 #define CLIPMI_EPI_STORE_PRE 128
+/* store the activation's derivative at the pre-activation to aux[m,n] (quick_gelu' with bit1,
+ * gelu_erf' with bit2), computed from the fp32 pre-activation beside the activation itself, so
+ * the backward is a plain product (bit9) instead of a load + derivative per element */
+#define CLIPMI_EPI_STORE_DACT 256
+/* C *= aux[m,n] (the stored derivative: d_pre = d_act * act'(pre)) */
+#define CLIPMI_EPI_MUL_AUX 512
 
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
 /* Diagnostic (no reference counterpart): arm / disarm (nullptr) the in-kernel s_memtime stamps of

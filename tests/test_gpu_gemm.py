@@ -19,6 +19,12 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
     if flags & _lib.EPI_BIAS:
         v = v + bias.float()
     pre = v.clone()
+    if flags & _lib.EPI_STORE_DACT:  # the activation's derivative at the pre-activation -> aux
+        if flags & _lib.EPI_QGELU:
+            sg = torch.sigmoid(1.702 * v)
+            pre = sg + 1.702 * v * sg * (1 - sg)
+        else:
+            pre = 0.5 * (1 + torch.erf(v / 2 ** 0.5)) + v * torch.exp(-0.5 * v * v) / (2 * torch.pi) ** 0.5
     if flags & _lib.EPI_QGELU:
         v = v * torch.sigmoid(1.702 * v)
     if flags & _lib.EPI_GELU:
@@ -27,6 +33,8 @@ def _ref_epi(acc, flags, bias=None, aux=None, res=None, cold=None, alpha=1.0):
         a = aux.float()
         s = torch.sigmoid(1.702 * a)
         v = v * (s + 1.702 * a * s * (1 - s))
+    if flags & _lib.EPI_MUL_AUX:
+        v = v * aux.float()
     if flags & _lib.EPI_RESID:
         v = v + res.float()
     if flags & _lib.EPI_BETA:
@@ -65,7 +73,9 @@ def test_gemm_layouts(dtype, akm, bkm, M, N, K, small):
 
 @pytest.mark.parametrize("flags", [
     _lib.EPI_BIAS, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, _lib.EPI_BIAS | _lib.EPI_GELU,
-    _lib.EPI_BIAS | _lib.EPI_RESID, _lib.EPI_DQGELU, _lib.EPI_BETA])
+    _lib.EPI_BIAS | _lib.EPI_RESID, _lib.EPI_DQGELU, _lib.EPI_BETA,
+    _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT, _lib.EPI_BIAS | _lib.EPI_GELU | _lib.EPI_STORE_DACT,
+    _lib.EPI_MUL_AUX])
 @pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("small", [0, 11])
 def test_gemm_epilogues(flags, cdtype, small):
@@ -85,7 +95,7 @@ def test_gemm_epilogues(flags, cdtype, small):
     torch.cuda.synchronize()
     tol = 3e-2 if cdtype == torch.bfloat16 else 1e-2
     assert (C.float() - ref).abs().max().item() / max(1.0, ref.abs().max().item()) < tol
-    if flags & _lib.EPI_STORE_PRE:
+    if flags & (_lib.EPI_STORE_PRE | _lib.EPI_STORE_DACT):
         assert (aux.float() - pre).abs().max().item() / max(1.0, pre.abs().max().item()) < tol
 
 
@@ -246,7 +256,8 @@ def test_layernorm_mxfp8(R, D):
 @pytest.mark.parametrize("bkm,flags", [
     (True, _lib.EPI_BIAS), (True, _lib.EPI_BIAS | _lib.EPI_RESID),
     (True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE), (True, _lib.EPI_BIAS | _lib.EPI_QGELU), (True, 0),
-    (False, 0), (False, _lib.EPI_DQGELU)])
+    (False, 0), (False, _lib.EPI_DQGELU),
+    (True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT), (False, _lib.EPI_MUL_AUX)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 776, 768), (520, 384, 128), (300, 264, 192),
                                    (2048, 512, 3072)])
 def test_gemm_4wave_matches_pingpong(var, bkm, flags, M, N, K):

@@ -16,6 +16,11 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("qkv_fwd", R, 2304, 768, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
     ("out_fwd", R, 768, 768, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
     ("fc2_dgrad", R, 3072, 768, True, False, torch.bfloat16, _lib.EPI_DQGELU, 1),
+    # the training path's forms since r03: fc1 stores quick_gelu'(pre), fc2's dgrad multiplies by it
+    ("fc1_fwd_dact", R, 3072, 768, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT, 1),
+    ("fc2_dgrad_ma", R, 3072, 768, True, False, torch.bfloat16, _lib.EPI_MUL_AUX, 1),
+    ("t_fc1_fwd_dact", RT, 2048, 512, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT, 1),
+    ("t_fc2_dgrad_ma", RT, 2048, 512, True, False, torch.bfloat16, _lib.EPI_MUL_AUX, 1),
     ("fc1_dgrad", R, 768, 3072, True, False, torch.bfloat16, 0, 1),
     ("qkv_dgrad", R, 768, 2304, True, False, torch.bfloat16, 0, 1),
     ("out_dgrad", R, 768, 768, True, False, torch.bfloat16, 0, 1),
@@ -68,7 +73,8 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     ldb = Kd if bkm else N
     C = torch.zeros(M, N, device="cuda", dtype=odt)
     bias = torch.randn(N, device="cuda").to(torch.bfloat16)
-    aux = torch.randn(M, N, device="cuda").to(odt) if flags & (_lib.EPI_DQGELU | _lib.EPI_STORE_PRE) else None
+    aux = (torch.randn(M, N, device="cuda").to(odt)
+           if flags & (_lib.EPI_DQGELU | _lib.EPI_STORE_PRE | _lib.EPI_STORE_DACT | _lib.EPI_MUL_AUX) else None)
     res = torch.randn(M, N, device="cuda").to(odt) if flags & _lib.EPI_RESID else None
     if split == 2:  # engine.cpp wgrad_splits: round efficiency minus the slabs' cost
         tiles = ((M + 255) // 256) * ((N + 255) // 256)

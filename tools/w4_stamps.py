@@ -22,7 +22,13 @@ SH = {"fc1_fwd": (R, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_
       # few-tile shapes (~60 workgroups = ~60 storing CUs): the epilogue's per-CU rate when the chip's
       # write bandwidth is not shared by all 256 CUs
       "qkv_fwd_60": (7 * 256, 2304, 768, True, _lib.EPI_BIAS),
-      "fc1_fwd_60": (5 * 256, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE)}
+      "fc1_fwd_60": (5 * 256, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE),
+      # fc1's epilogue without the pre-activation store / without the gelu as well
+      "fc1_fwd_nopre": (R, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU),
+      "fc1_fwd_bias": (R, 3072, 768, True, _lib.EPI_BIAS),
+      "fc2_dgrad": (R, 3072, 768, False, _lib.EPI_DQGELU), "fc2_dgrad_plain": (R, 3072, 768, False, 0),
+      "fc1_fwd_dact": (R, 3072, 768, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT),
+      "fc2_dgrad_ma": (R, 3072, 768, False, _lib.EPI_MUL_AUX)}
 _lib.declare("clipmi_gemm_stamps", [ctypes.c_void_p])
 L = _lib.lib()
 buf = torch.zeros(512 * 4 * 128, dtype=torch.int64, device="cuda")

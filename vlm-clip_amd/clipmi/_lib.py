@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("CLIPMI_LIB") or os.path.join(_HERE, "libclipmi.so")
 F32, BF16, FP8 = 0, 1, 2
 EPI_BIAS, EPI_QGELU, EPI_GELU, EPI_RESID = 1, 2, 4, 8
 EPI_DQGELU, EPI_DGELU, EPI_BETA, EPI_STORE_PRE = 16, 32, 64, 128
+EPI_STORE_DACT, EPI_MUL_AUX = 256, 512
 
 c_i64 = ctypes.c_int64
 c_vp = ctypes.c_void_p

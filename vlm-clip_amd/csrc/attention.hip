@@ -930,6 +930,288 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   }
 }
 
+// ------------------------------------------------------------------- bwd, single pass
+// attn_bwd_sp<CAUSAL, NW, NKC>: the backward of one (batch, head) item in ONE sweep over its query
+// steps (32 queries each), N <= 32 * NKC.  attn_bwd_pf computes dK/dV in a key-owned phase and dQ
+// in a query-owned phase, recomputing S, dP and every exponential for the second; here:
+//   per step qs, every wave: S = Q K^T and dP = dO V^T of its key blocks against the step's
+//   queries (Q/dO fragments from the LDS images, K/V fragments in registers), P and
+//   dS = P (dP - delta), dV += P^T dO and dK += dS^T Q in registers (as attn_bwd_pf's phase A), and
+//   dS^T (the bf16 values dK used) into one 32-column half of a [NPAD keys][64] dS image;
+//   one barrier; then dQ^T(step) = K^T dS^T over all NPAD keys: wave w owns the (d-tile, query
+//   half) tile(s) of the step's [32 x 64] dQ block -- one with 8 waves, two with 4 -- from K^T
+//   fragments held in registers for the whole item, and writes it out.  The two dS halves
+//   alternate between steps, so one barrier per step covers both hazards.
+// So per (16 queries x 32 keys) the MFMA count drops from 28 to 20 and the exponentials halve.
+// Next item's operands: its K image DMA'd into the second K slot and its V fragments loaded into
+// registers at the start of this item; the Q / dO rows of step qs DMA'd right after the barrier
+// that retires them (rolling); O rows (for delta = rowsum(dO o O)) and lse / key mask prefetched
+// into registers.  K and K^T fragments are read from the K image where they are used (two
+// waves per SIMD leave 256 registers per wave: holding them for the whole item spilled).
+// LDS: Q, dO, K x 2, dS images (5 x NPAD x 128 B) + 2 slots of lse2 | delta | keyok.
+template <bool CAUSAL, int NW, int NKC>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_sp(AttnP p, int nitems) {  // 2 waves per SIMD
+  constexpr int NT = NW * 64, NPAD = NKC * 32, IMG = NPAD * 128;
+  constexpr int NB = 2;                                  // key blocks per wave (nkb <= 2 NW)
+  constexpr int NQT = 8 / NW;                            // dQ tiles per wave per step
+  constexpr int NOC = (NPAD * 8 + NT - 1) / NT;          // O chunks per thread (delta)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int N = p.N, D = p.D, H = p.H;
+  const int64_t ld = 3 * (int64_t)D;
+  char* Qimg = smem;
+  char* dOimg = smem + IMG;
+  char* Kimg2 = smem + 2 * IMG;  // [2 slots]
+  char* dSimg = smem + 4 * IMG;
+  float* arr = (float*)(smem + 5 * IMG);  // [2 slots][lse2 | delta | keyok][NPAD]
+  const uint32_t rec3 = (uint32_t)((int64_t)(N - 1) * ld * 2 + 128);
+  const uint32_t rec1 = (uint32_t)((int64_t)(N - 1) * D * 2 + 128);
+  const float c2 = p.scale * LOG2E;
+  const int g = lane >> 4, li = lane & 15;
+  const int nkb = (N + 15) >> 4, nstep = (N + 31) >> 5;
+  const int dt = wave & 3;  // this wave's dQ d-tile
+
+  auto qkv_of = [&](int item) {
+    const int b = item / H, h = item - b * H;
+    return p.qkv + (int64_t)b * N * ld + h * 64;
+  };
+  auto issue_k = [&](int item, int slot) {
+    const SRsrc rk = make_srsrc(qkv_of(item) + D, rec3);
+    char* kimg = Kimg2 + __builtin_amdgcn_readfirstlane(slot * IMG);  // wave-uniform M0 base
+#pragma unroll 1
+    for (int j = wave; j < NPAD / 8; j += NW) {
+      const int r = 8 * j + (lane >> 3), c = ((lane & 7) ^ (r & 6)) << 4;
+      dma16(rk, kimg + j * 1024, r * (int)ld * 2 + c);
+    }
+  };
+  auto load_vf = [&](int item, bf16x8 (&vf)[NB][2]) {  // V fragments of the wave's key blocks
+    const bf16* base = qkv_of(item) + 2 * D;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int key = min((wave + NW * u) * 16 + li, N - 1);  // rows past N are masked by keyok
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) vf[u][kk] = *(const bf16x8*)(base + (int64_t)key * ld + kk * 32 + 8 * g);
+    }
+  };
+  // Q / dO rows [8 j0, 8 j1) of item (1 KiB pieces of 8 rows)
+  auto issue_qdo = [&](int item, int j0, int j1) {
+    const int b = item / H, h = item - b * H;
+    const SRsrc rq = make_srsrc(qkv_of(item), rec3);
+    const SRsrc rd = make_srsrc(p.dout + (int64_t)b * N * D + h * 64, rec1);
+#pragma unroll 1
+    for (int j = j0 + wave; j < j1; j += NW) {
+      const int r = 8 * j + (lane >> 3), c = ((lane & 7) ^ (r & 6)) << 4;
+      dma16(rq, Qimg + j * 1024, r * (int)ld * 2 + c);
+      dma16(rd, dOimg + j * 1024, r * D * 2 + c);
+    }
+  };
+  auto load_o = [&](int item, u32x4 (&o)[NOC]) {
+    const int b = item / H, h = item - b * H;
+    const bf16* base = p.o + (int64_t)b * N * D + h * 64;
+#pragma unroll
+    for (int j = 0; j < NOC; ++j) {
+      const int id = t + NT * j, r = id >> 3, c = id & 7;
+      o[j] = u32x4{0u, 0u, 0u, 0u};
+      if (id < NPAD * 8 && r < N) o[j] = *(const u32x4*)(base + (int64_t)r * D + c * 8);
+    }
+  };
+  auto load_meta = [&](int item, float& l2v, int& kov) {
+    const int b = item / H, h = item - b * H;
+    l2v = __builtin_huge_valf();
+    kov = 0;
+    if (t < N) {
+      l2v = p.lse[((int64_t)b * H + h) * N + t] * LOG2E;
+      kov = !p.kmask || p.kmask[(int64_t)b * N + t] != 0;
+    }
+  };
+  static_assert(NPAD <= NT, "one thread per key / query row");
+  auto store_meta = [&](int sl, float l2v, int kov) {
+    if (t < NPAD) {
+      arr[sl * 3 * NPAD + t] = l2v;
+      ((int*)arr)[sl * 3 * NPAD + 2 * NPAD + t] = kov;
+    }
+  };
+
+  int item = blockIdx.x;
+  u32x4 orow[NOC];
+  bf16x8 vfn[NB][2];
+  {
+    float l2v;
+    int kov;
+    issue_k(item, 0);
+    load_vf(item, vfn);
+    issue_qdo(item, 0, NPAD / 8);
+    load_o(item, orow);
+    load_meta(item, l2v, kov);
+    for (int id = t; id < NPAD * 8; id += NT) *LDS_PTR(u32x4, dSimg + id * 16) = u32x4{0u, 0u, 0u, 0u};
+    store_meta(0, l2v, kov);
+  }
+  for (int it = 0;; ++it) {
+    const int sl = it & 1;
+    const float* lse2 = arr + sl * 3 * NPAD;
+    float* delta = arr + sl * 3 * NPAD + NPAD;
+    const int* keyok = (const int*)(arr + sl * 3 * NPAD + 2 * NPAD);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // item's images, meta and O rows landed; the dS image idle
+    const int cur = item, nxt = item + gridDim.x;
+    const bool more = nxt < nitems;
+    const int b = cur / H, h = cur - b * H;
+    bf16* dq_base = p.dqkv + (int64_t)b * N * ld + h * 64;
+
+    const char* Kimg = Kimg2 + __builtin_amdgcn_readfirstlane(sl * IMG);
+    int key[NB], krow[NB];
+    bool kok[NB], kbv[NB];
+    bf16x8 vf[NB][2];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int kb = wave + NW * u;
+      kbv[u] = kb < nkb;
+      key[u] = kb * 16 + li;
+      krow[u] = min(key[u], NPAD - 1);
+      kok[u] = keyok[krow[u]] != 0;
+      vf[u][0] = vfn[u][0];
+      vf[u][1] = vfn[u][1];
+    }
+    // delta[q] = sum_d dO * O, 8 lanes per row (dO image, O rows in registers)
+#pragma unroll
+    for (int j = 0; j < NOC; ++j) {
+      const int id = t + NT * j, r = id >> 3, c = id & 7;
+      if (NOC * NT == NPAD * 8 || id < NPAD * 8) {  // whole 8-lane groups: NPAD * 8 % 8 == 0
+        const bf16x8 a = frag_row(dOimg, r, c);
+        float sum = 0.f;
+        const u32x4 o4 = orow[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sum = fmaf((float)a[2 * e], __uint_as_float(o4[e] << 16), sum);
+          sum = fmaf((float)a[2 * e + 1], __uint_as_float(o4[e] & 0xffff0000u), sum);
+        }
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        sum += __shfl_xor(sum, 4, 64);
+        if (c == 0) delta[r] = sum;
+      }
+    }
+    raw_barrier_lds();  // delta visible (the other K slot's readers, item it - 1, are done)
+    float l2n = 0.f;
+    int kon = 0;
+    if (more) {
+      issue_k(nxt, sl ^ 1);
+      load_vf(nxt, vfn);
+      load_o(nxt, orow);
+      load_meta(nxt, l2n, kon);
+    }
+
+    f32x4 dv[NB][4], dk[NB][4];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) { dv[u][v] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u][v] = dv[u][v]; }
+
+    for (int qs = 0; qs < nstep; ++qs) {
+      const int hb = qs & 1;
+      bool act[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) act[u] = kbv[u] && !(CAUSAL && qs * 32 + 31 < (wave + NW * u) * 16);
+      // P and dS of each key block, packed to bf16 per 16-query half (tau) as soon as they are
+      // formed; dS^T goes to the dS image at once (zeros for a causally skipped block)
+      bf16x4 pl[NB][2], sl[NB][2];
+#pragma unroll
+      for (int tau = 0; tau < 2; ++tau) {
+        const int qr = qs * 32 + tau * 16 + li;
+        bf16x8 qa[2], da[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          qa[kk] = frag_row(Qimg, qr, kk * 4 + g);
+          da[kk] = frag_row(dOimg, qr, kk * 4 + g);
+        }
+        const int q0 = qs * 32 + tau * 16 + 4 * g;
+        const f32x4 l4 = *LDS_PTR(const f32x4, lse2 + q0);
+        const f32x4 d4 = *LDS_PTR(const f32x4, delta + q0);
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          float pv4[4] = {0.f, 0.f, 0.f, 0.f}, ds4[4] = {0.f, 0.f, 0.f, 0.f};
+          if (act[u]) {
+            f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+              const bf16x8 kf = frag_row(Kimg, krow[u], kk * 4 + g);
+              sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kf, sc, 0, 0, 0);
+              dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[kk], vf[u][kk], dp, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const bool ok = kok[u] && (!CAUSAL || key[u] <= q0 + r);
+              pv4[r] = ok ? __builtin_amdgcn_exp2f(sc[r] * c2 - l4[r]) : 0.f;
+              ds4[r] = pv4[r] * (dp[r] - d4[r]);
+            }
+          }
+          pl[u][tau] = bf16x4{(bf16)pv4[0], (bf16)pv4[1], (bf16)pv4[2], (bf16)pv4[3]};
+          sl[u][tau] = bf16x4{(bf16)ds4[0], (bf16)ds4[1], (bf16)ds4[2], (bf16)ds4[3]};
+          if (kbv[u])  // dS^T row key[u], columns hb*32 + tau*16 + 4g .. +3
+            *LDS_PTR(bf16x4, dSimg + img_off(key[u], hb * 4 + tau * 2 + (g >> 1)) + (g & 1) * 8) = sl[u][tau];
+        }
+      }
+      bf16x8 pf[NB], sf[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        pf[u] = bf16x8{pl[u][0][0], pl[u][0][1], pl[u][0][2], pl[u][0][3], pl[u][1][0], pl[u][1][1], pl[u][1][2], pl[u][1][3]};
+        sf[u] = bf16x8{sl[u][0][0], sl[u][0][1], sl[u][0][2], sl[u][0][3], sl[u][1][0], sl[u][1][1], sl[u][1][2], sl[u][1][3]};
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const bf16x8 td = frag_tr(dOimg, qs * 32, v * 16, lane), tq = frag_tr(Qimg, qs * 32, v * 16, lane);
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          if (!act[u]) continue;
+          dv[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(td, pf[u], dv[u][v], 0, 0, 0);
+          dk[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tq, sf[u], dk[u][v], 0, 0, 0);
+        }
+      }
+      raw_barrier_lds();  // dS(qs) complete; every wave done with step qs's Q / dO rows
+      if (more) issue_qdo(nxt, qs * 4, qs * 4 + 4);
+      // dQ^T of step qs: this wave's tile(s) over all keys (causal: keys <= the step's last query)
+      const int kcl = CAUSAL ? min(NKC, qs + 1) : NKC;
+#pragma unroll
+      for (int j = 0; j < NQT; ++j) {
+        const int qt = NQT == 1 ? (wave >> 2) : j;
+        // two independent accumulation chains (even / odd key chunks): half the dependent MFMA latency
+        f32x4 acc2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          if (kc < kcl) {
+            const bf16x8 kt = frag_tr(Kimg, kc * 32, dt * 16, lane);
+            const bf16x8 st = frag_tr(dSimg, kc * 32, hb * 32 + qt * 16, lane);
+            acc2[kc & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, st, acc2[kc & 1], 0, 0, 0);
+          }
+        }
+        const f32x4 acc = acc2[0] + acc2[1];
+        const int q = qs * 32 + qt * 16 + li;
+        if (q < N) {
+          float a[4] = {acc[0] * p.scale, acc[1] * p.scale, acc[2] * p.scale, acc[3] * p.scale};
+          store4(dq_base + (int64_t)q * ld + dt * 16 + 4 * g, a);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      if (kbv[u] && key[u] < N) {
+        bf16* row = dq_base + (int64_t)key[u] * ld;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float a[4] = {dk[u][v][0] * p.scale, dk[u][v][1] * p.scale, dk[u][v][2] * p.scale, dk[u][v][3] * p.scale};
+          float w[4] = {dv[u][v][0], dv[u][v][1], dv[u][v][2], dv[u][v][3]};
+          store4(row + D + v * 16 + 4 * g, a);
+          store4(row + 2 * D + v * 16 + 4 * g, w);
+        }
+      }
+    }
+    if (!more) break;
+    store_meta(sl ^ 1, l2n, kon);  // slot sl ^ 1's readers (item it - 1) finished long ago
+    item = nxt;
+  }
+}
+
 // ------------------------------------------------------------------ fwd, K/V streaming
 // Flash-attention forward for any N (ViT-L/14@336: N = 577 does not fit the whole-K/V kernel
 // above).  One 4-wave workgroup per (batch, head, chunk of FA_QC(QPW) queries); two or more
@@ -1382,9 +1664,38 @@ void launch_bwd_pf(const AttnP& p, hipStream_t s) {
   const int grid = std::min(nitems, 256 * per_cu);
   hipLaunchKernelGGL((attn_bwd_pf<C, NW>), dim3(grid), dim3(NW * 64), lds, s, p, nitems);
 }
+template <bool C, int NW, int NKC>
+void launch_bwd_sp(const AttnP& p, hipStream_t s) {
+  constexpr size_t lds = 5 * (size_t)NKC * 32 * 128 + 6 * (size_t)NKC * 32 * 4;
+  static_assert(lds <= 160 * 1024, "attn_bwd_sp: LDS");
+  (void)lds_optin((const void*)attn_bwd_sp<C, NW, NKC>, (int)lds);
+  const int nitems = p.B * p.H;
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+  const int grid = std::min(nitems, 256 * per_cu);
+  hipLaunchKernelGGL((attn_bwd_sp<C, NW, NKC>), dim3(grid), dim3(NW * 64), lds, s, p, nitems);
+}
+template <bool C>
+int bwd_sp_dispatch(const AttnP& p, hipStream_t s) {
+  switch ((p.N + 31) >> 5) {  // 8 waves (ViT-B/16: N = 197, 7 steps)
+    case 5: launch_bwd_sp<C, 8, 5>(p, s); return CLIPMI_OK;
+    case 6: launch_bwd_sp<C, 8, 6>(p, s); return CLIPMI_OK;
+    case 7: launch_bwd_sp<C, 8, 7>(p, s); return CLIPMI_OK;
+    default: return clipmi_invalid("attn_bwd_sp: N must be in (128, 224]");
+  }
+}
+// the single-pass backward for 128 < N <= 224 unless CLIPMI_ATTN_BWD_SP=0 (A/B hook, read per
+// call).  (Its 4-wave form for the text tower, N = 77 with the causal mask, spilled at the 256
+// registers two workgroups per CU leave, so the text tower keeps attn_bwd_pf.)
+static bool use_bwd_sp(int N) {
+  if (N <= 128 || N > 224) return false;
+  const char* e = getenv("CLIPMI_ATTN_BWD_SP");
+  return !e || atoi(e) != 0;
+}
+
 // 4 waves per workgroup for N <= 128 (text: 5 blocks of 16 rows), else 8; each wave owns at
 // most 2 key blocks and 2 query blocks.
 int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
+  if (use_bwd_sp(p.N)) return causal ? bwd_sp_dispatch<true>(p, s) : bwd_sp_dispatch<false>(p, s);
   // CLIPMI_ATTN_BWD_NW=16 (A/B hook, read per call): one block per wave, 4 waves per SIMD.  Measured
   // 3-5 % slower than 8 waves at N = 197 (profiles/r02_attn_waves_ab.log): this backward is bound by
   // its LDS fragment traffic (each wave re-reads the Q/dO and K/V fragments of every step), which

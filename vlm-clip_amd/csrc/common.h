@@ -26,7 +26,11 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 
 // sigmoid(1.702 x) through v_exp + v_rcp (1 ulp) instead of an IEEE division sequence:
 // these run per output element in the GEMM epilogues
-__device__ __forceinline__ float qg_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x)); }
+// sigmoid(1.702 x) = 1 / (1 + 2^(x * -1.702 log2 e)): one multiply before v_exp_f32 (the
+// epilogues of the quick_gelu GEMMs are VALU-bound on this: profiles/r03_epilogue_stamps.log)
+__device__ __forceinline__ float qg_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * (-1.702f * 1.4426950408889634f)));
+}
 __device__ __forceinline__ float quick_gelu(float x) { return x * qg_sigmoid(x); }
 __device__ __forceinline__ float quick_gelu_grad(float x) {
   const float s = qg_sigmoid(x);

@@ -215,7 +215,9 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
                     w.out_b, a.x_in, D));
     CLIPMI_TRY(clipmi_layernorm_fwd(s, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
                                     nullptr, nullptr, 0));
-    const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_PRE : 0);
+    // training: a.pre receives quick_gelu'(pre) (computed beside the activation from the fp32
+    // pre-activation), so fc2's input gradient below is one product per element
+    const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_DACT : 0);
     CLIPMI_TRY(gemm(s, dt, R, F, D, a.ln2, D, true, w.fc1_w, D, true, a.act, F, dt, f1, w.fc1_b, nullptr, 0, a.pre, F));
     CLIPMI_TRY(gemm(s, dt, R, D, F, a.act, F, true, w.fc2_w, F, true, x_out, D, dt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
                     w.fc2_b, a.h, D));
@@ -270,7 +272,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     const clipmi_layer_grad& g = d->grads[l];
     CLIPMI_REQUIRE(a.pre, "training forward must save pre-activations");
     // MLP branch: dx is dL/dy
-    CLIPMI_TRY(gemm(s, dt, R, F, D, dx, D, true, w.fc2_w, F, false, dbig, F, dt, CLIPMI_EPI_DQGELU, nullptr, nullptr,
+    CLIPMI_TRY(gemm(s, dt, R, F, D, dx, D, true, w.fc2_w, F, false, dbig, F, dt, CLIPMI_EPI_MUL_AUX, nullptr, nullptr,
                     0, a.pre, F));                                          // d_pre = (dx W2) * qgelu'(pre)
     CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w, g.fc2_b));            // gW2 += dx^T act, gb2 += sum dx
     CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w, g.fc1_b));          // gW1 += d_pre^T ln2

@@ -1244,6 +1244,7 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
 
 constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU, E_G = CLIPMI_EPI_GELU;
 constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU, E_DG = CLIPMI_EPI_DGELU, E_BETA = CLIPMI_EPI_BETA;
+constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
 
 const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
   if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
@@ -1279,6 +1280,7 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
       case E_B: launch256<true, true, bf16, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias";
       case E_B | E_R: launch256<true, true, bf16, E_B | E_R, false>(p, splits, s, bg); return "gemm256_fwd_bias_resid";
       case E_B | E_Q | E_P: launch256<true, true, bf16, E_B | E_Q | E_P, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu_pre";
+      case E_B | E_Q | E_DA: launch256<true, true, bf16, E_B | E_Q | E_DA, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu_dact";
       case E_B | E_Q: launch256<true, true, bf16, E_B | E_Q, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu";
       case 0: launch256<true, true, bf16, 0, false>(p, splits, s, bg); return "gemm256_fwd";
       default: break;
@@ -1288,6 +1290,7 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     switch (flags) {
       case 0: launch256<true, false, bf16, 0, false>(p, splits, s, bg); return "gemm256_dgrad";
       case E_DQ: launch256<true, false, bf16, E_DQ, false>(p, splits, s, bg); return "gemm256_dgrad_dqgelu";
+      case E_MA: launch256<true, false, bf16, E_MA, false>(p, splits, s, bg); return "gemm256_dgrad_mulaux";
       default: break;
     }
   }
@@ -1372,6 +1375,17 @@ extern "C" int clipmi_gemm_stamps(void* buf) {
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
+  // every operand an epilogue flag reads or writes must be given (a null one would fault the GPU)
+  {
+    constexpr int AUXF = CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU | CLIPMI_EPI_STORE_PRE | CLIPMI_EPI_STORE_DACT |
+                         CLIPMI_EPI_MUL_AUX;
+    CLIPMI_REQUIRE(!(d->flags & AUXF) || (d->aux && d->ldaux >= d->N), "epilogue flags need aux (ldaux >= N)");
+    CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_RESID) || (d->residual && d->ldr >= d->N), "residual flag needs residual (ldr >= N)");
+    CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_BIAS) || d->bias, "bias flag needs bias");
+    CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_STORE_DACT) || (d->flags & (CLIPMI_EPI_QGELU | CLIPMI_EPI_GELU)),
+                   "store_dact needs an activation flag");
+    CLIPMI_REQUIRE((d->flags & ~1023) == 0, "unknown epilogue flag");
+  }
   if (d->ab_dtype == CLIPMI_FP8) {  // MXFP8 operands (see include/clipmi.h)
     CLIPMI_REQUIRE(d->a_kmajor && d->b_kmajor, "fp8: both operands k-major");
     CLIPMI_REQUIRE(d->K % 128 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0, "fp8: K % 128 == 0, lda/ldb % 16 == 0");

@@ -317,8 +317,7 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
   // every wave passed the last step's barrier after its last useful LDS read and DMA: the stages
   // are idle, so the epilogue may stage rows in this wave's 16 KiB of them
   char* st = smem + wave * 16384;
-  finish256<OutT, EPI, true>(p, acc[0], m0 + wm * 128, n0 + wn * 128, lane, 0, st);
-  finish256<OutT, EPI, true>(p, acc[1], m0 + wm * 128, n0 + wn * 128 + 64, lane, 0, st);
+  finish256x2<OutT, EPI, true>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, 0, st);
   if (ST) {
     const unsigned long long st_end = __builtin_amdgcn_s_memtime();
     const unsigned long long st_real1 = __builtin_amdgcn_s_memrealtime();
@@ -429,8 +428,7 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
       }
     }
     char* st = smem + 2 * W4_STAGE + wave * 8192;
-    finish256<OutT, EPI, true>(p, acc[0], m0 + wm * 128, n0 + wn * 128, lane, kz, st);
-    finish256<OutT, EPI, true>(p, acc[1], m0 + wm * 128, n0 + wn * 128 + 64, lane, kz, st);
+    finish256x2<OutT, EPI, true>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, kz, st);
     if (next >= nitems) break;
     item = next;
   }
@@ -474,11 +472,13 @@ void launch_w4(const GemmP& p, hipStream_t s, int dm) {
 const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int dm) {
   constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU;
   constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU;
+  constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
   if (bkm) {
     switch (flags) {
       case E_B: launch_w4<true, E_B>(p, s, dm); return "gemm256_fwd_bias";
       case E_B | E_R: launch_w4<true, E_B | E_R>(p, s, dm); return "gemm256_fwd_bias_resid";
       case E_B | E_Q | E_P: launch_w4<true, E_B | E_Q | E_P>(p, s, dm); return "gemm256_fwd_bias_qgelu_pre";
+      case E_B | E_Q | E_DA: launch_w4<true, E_B | E_Q | E_DA>(p, s, dm); return "gemm256_fwd_bias_qgelu_dact";
       case E_B | E_Q: launch_w4<true, E_B | E_Q>(p, s, dm); return "gemm256_fwd_bias_qgelu";
       case 0: launch_w4<true, 0>(p, s, dm); return "gemm256_fwd";
       default: return nullptr;
@@ -487,6 +487,7 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
   switch (flags) {
     case 0: launch_w4<false, 0>(p, s, dm); return "gemm256_dgrad";
     case E_DQ: launch_w4<false, E_DQ>(p, s, dm); return "gemm256_dgrad_dqgelu";
+    case E_MA: launch_w4<false, E_MA>(p, s, dm); return "gemm256_dgrad_mulaux";
     default: return nullptr;
   }
 }

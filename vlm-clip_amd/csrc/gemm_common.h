@@ -85,6 +85,12 @@ __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[
     for (int j = 0; j < 4; ++j) v[j] += j < nv ? ld_bias(p, n + j) : 0.f;
   }
   if (f & CLIPMI_EPI_STORE_PRE) st4((OutT*)p.aux + (int64_t)m * p.ldaux + n, v, nv, vec);
+  if (f & CLIPMI_EPI_STORE_DACT) {
+    float d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = (f & CLIPMI_EPI_QGELU) ? quick_gelu_grad(v[j]) : gelu_erf_grad(v[j]);
+    st4((OutT*)p.aux + (int64_t)m * p.ldaux + n, d, nv, vec);
+  }
   if (f & CLIPMI_EPI_QGELU) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
@@ -102,6 +108,12 @@ __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float v[
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] *= gelu_erf_grad(a[j]);
     }
+  }
+  if (f & CLIPMI_EPI_MUL_AUX) {
+    float a[4];
+    ld4((const OutT*)p.aux + (int64_t)m * p.ldaux + n, a, nv, vec);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] *= a[j];
   }
   if (f & CLIPMI_EPI_RESID) {
     float r[4];
@@ -544,6 +556,167 @@ __device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][
   }
 }
 
+#ifndef CLIPMI_EPI_PD
+#define CLIPMI_EPI_PD 4
+#endif
+// 8 bf16 packed in 4 dwords -> float (element 2i in the low half of dword i)
+__device__ __forceinline__ void unpack8(const u32x4& x, float v[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(x[i] << 16);
+    v[2 * i + 1] = __uint_as_float(x[i] & 0xffff0000u);
+  }
+}
+
+// Pipelined form of epilogue256_lds over a wave's NC adjacent 128x64 blocks (NC = 1: the 8-wave
+// kernels' block, NC = 2: the 4-wave kernel's 128x128), in parts of 64 rows x 64 columns, each
+// staged through the wave's 8 KiB of LDS.  Same math and rounding as epilogue256_lds.  Measured
+// problem it removes (profiles/r03_epilogue_isa.txt, in-kernel stamps): a part's store chain was
+// ds_read -> s_waitcnt lgkmcnt(0) -> global_store per instruction, and every input load issued
+// after a store waited for that store's write acknowledgement (vmcnt counts loads and stores in
+// issue order), so the epilogue ran ~9 B/clk per CU whether 60 or 256 CUs were storing.  Here:
+//  * every bias value is loaded once, before any store, and each part's residual / pre-activation
+//    / old-C inputs are loaded before the previous part's stores (double-buffered raw registers);
+//  * a part's 8 staged row groups are read back in one batch, then stored;
+//  * full tiles (every CLIP shape) store with no per-row exec branches.
+template <int EPI, bool AR, int NC>
+__device__ __forceinline__ void epilogue_lds_pipe(const GemmP& p, f32x4 (&acc)[NC][8][4], int mb, int nb, int lane,
+                                                  char* st) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
+  constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
+  constexpr bool HDA = EPI & CLIPMI_EPI_STORE_DACT, HMA = EPI & CLIPMI_EPI_MUL_AUX;
+  constexpr bool HAUX = HDQ || HDG || HMA;
+  constexpr bool HIN = HR || HAUX || HBETA;
+  constexpr bool H2 = HPRE || HDA;  // a second output (aux), staged through LDS after the first
+  constexpr int NPART = 2 * NC;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);
+  const bool full = mb + 128 <= p.M && nb + 64 * NC <= p.N;
+  float bv[NC][2][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int n = min(nb + 64 * c + 32 * jp + coff, p.N - 8);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bv[c][jp][r] = 0.f;
+      if (HB) {
+        if (p.bias_f32) {
+          load4((const float*)p.bias + n, bv[c][jp]);
+          load4((const float*)p.bias + n + 4, bv[c][jp] + 4);
+        } else {
+          load8((const bf16*)p.bias + n, bv[c][jp]);
+        }
+      }
+    }
+  const bf16* src = HR ? (const bf16*)p.res : HAUX ? (const bf16*)p.aux : (const bf16*)p.C;
+  const int64_t lds_in = HR ? p.ldr : HAUX ? p.ldaux : p.ldc;
+  // inputs PD parts ahead (default: every part, issued before the first store)
+  constexpr int PD = CLIPMI_EPI_PD > 0 ? (CLIPMI_EPI_PD < NPART ? CLIPMI_EPI_PD : NPART) : NPART;
+  u32x4 xr[PD][4][2];
+  auto load_in = [&](int part, u32x4 (&x)[4][2]) {
+    const int c = part >> 1, h = part & 1;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int n = min(nb + 64 * c + 32 * jp + coff, p.N - 8);
+        x[ii][jp] = *(const u32x4*)(src + (int64_t)m * lds_in + n);
+      }
+    }
+  };
+  if (HIN) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) load_in(q, xr[q]);
+  }
+#pragma unroll
+  for (int part = 0; part < NPART; ++part) {
+    const int c = part >> 1, h = part & 1;
+    u32x4 aux2[4][2];  // the part's second output (pre-activation or its derivative), packed bf16
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = h * 4 + ii;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        float v[8];
+        // AGPR accumulators (4-wave kernel): a scheduling fence per fragment pair instead of
+        // acc_pin, whose "+a" redefinition made the compiler copy every pair into a0..a7 before
+        // reading it (56 v_accvgpr_mov per part); the fence alone keeps the reads in place, unspilled
+        if constexpr (AR) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[c][i][2 * jp][r]),
+                                                           __float_as_uint(acc[c][i][2 * jp + 1][r]), false, false);
+          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[c][jp][r];
+          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[c][jp][r + 4];
+        }
+        float xin[8], w2[8];
+        if (HIN) unpack8(xr[part % PD][ii][jp], xin);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (HPRE) w2[r] = v[r];
+          if (HQ) {
+            const float sg = qg_sigmoid(v[r]);  // one exp + rcp for quick_gelu and its derivative
+            if (HDA) {  // s + 1.702 x s (1 - s) = s (1 + t - t s), t = 1.702 x
+              const float tq = 1.702f * v[r];
+              w2[r] = fmaf(sg, fmaf(-tq, sg, tq), sg);
+            }
+            v[r] *= sg;
+          }
+          if (HG) {
+            if (HDA) w2[r] = gelu_erf_grad(v[r]);
+            v[r] = gelu_erf(v[r]);
+          }
+          if (HDQ) v[r] *= quick_gelu_grad(xin[r]);
+          if (HDG) v[r] *= gelu_erf_grad(xin[r]);
+          if (HMA) v[r] *= xin[r];
+          if (HR || HBETA) v[r] += xin[r];
+        }
+        if (H2)
+          aux2[ii][jp] = __builtin_bit_cast(u32x4, bf16x8{(bf16)w2[0], (bf16)w2[1], (bf16)w2[2], (bf16)w2[3],
+                                                           (bf16)w2[4], (bf16)w2[5], (bf16)w2[6], (bf16)w2[7]});
+        *LDS_PTR(bf16x8, st + stage_off(ii * 16 + mlane, (32 * jp + coff) >> 3)) =
+            bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+      }
+    }
+    if (HIN && part + PD < NPART) load_in(part + PD, xr[part % PD]);  // before this part's stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                    // this wave's staging writes landed
+    u32x4 o[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) o[it] = *LDS_PTR(const u32x4, st + stage_off(it * 8 + (lane >> 3), lane & 7));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next part overwrites
+    if (H2) {  // the second output into the staging buffer, now that its read-back landed
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) *LDS_PTR(u32x4, st + stage_off(ii * 16 + mlane, (32 * jp + coff) >> 3)) = aux2[ii][jp];
+    }
+    const int r0 = mb + h * 64 + (lane >> 3), col = nb + 64 * c + (lane & 7) * 8;
+    auto store_rows = [&](bf16* base, int64_t ld, const u32x4 (&rows)[8]) {
+      bf16* out = base + (int64_t)r0 * ld + col;
+      const int64_t step = 8 * ld;
+      if (full) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) *(u32x4*)(out + it * step) = rows[it];
+      } else {
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+          if (r0 + it * 8 < p.M && col < p.N) *(u32x4*)(out + it * step) = rows[it];
+      }
+    };
+    store_rows((bf16*)p.C, p.ldc, o);
+    if (H2) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 8; ++it) o[it] = *LDS_PTR(const u32x4, st + stage_off(it * 8 + (lane >> 3), lane & 7));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      store_rows((bf16*)p.aux, p.ldaux, o);
+    }
+  }
+}
+
 // Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
 // allows it (4-aligned columns, aligned leading dims; the 16-B form for bf16 output when
 // columns, leading dims and pointers allow 16-B accesses), else the per-subtile generic path
@@ -553,9 +726,24 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
                                           char* stage = nullptr) {
   constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
                         !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
-  if constexpr (FAST && std::is_same<OutT, bf16>::value) {
+  // the derivative-store / aux-product flags have a fast form only in the pipelined LDS epilogue
+  constexpr bool NEWF = EPI >= 0 && (EPI & (CLIPMI_EPI_STORE_DACT | CLIPMI_EPI_MUL_AUX));
+  if constexpr (NEWF) {
+#if !CLIPMI_OLD_EPI
+    if constexpr (std::is_same<OutT, bf16>::value) {
+      if (stage && !p.ws && p.vec8) {
+        epilogue_lds_pipe<EPI, AR, 1>(p, reinterpret_cast<f32x4(&)[1][8][4]>(acc), mb, nb, lane, stage);
+        return;
+      }
+    }
+#endif
+  } else if constexpr (FAST && std::is_same<OutT, bf16>::value) {
     if (stage && !p.ws && p.vec8) {
+#if CLIPMI_OLD_EPI
       epilogue256_lds<EPI < 0 ? 0 : EPI, AR>(p, acc, mb, nb, lane, stage);
+#else
+      epilogue_lds_pipe<EPI < 0 ? 0 : EPI, AR, 1>(p, reinterpret_cast<f32x4(&)[1][8][4]>(acc), mb, nb, lane, stage);
+#endif
       return;
     }
     if (!p.ws && p.vec8) {
@@ -563,7 +751,7 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
       return;
     }
   }
-  if (FAST && !p.ws && p.vec && (p.N & 3) == 0) {
+  if (FAST && !NEWF && !p.ws && p.vec && (p.N & 3) == 0) {
     epilogue256<OutT, EPI < 0 ? 0 : EPI, AR>(p, acc, mb, nb, lane);
     return;
   }
@@ -581,6 +769,26 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
       else epilogue4<OutT, EPI>(p, m, n, v);
     }
   }
+}
+
+// The 4-wave kernel's 128x128 wave block (two 128x64 halves): one pipelined LDS epilogue over
+// both halves where finish256 would stage through LDS (so the second half's bias / input loads
+// are not issued behind the first half's stores), else finish256 per half.
+template <typename OutT, int EPI, bool AR>
+__device__ __forceinline__ void finish256x2(const GemmP& p, f32x4 (&acc)[2][8][4], int mb, int nb, int lane, int kz,
+                                            char* stage) {
+  constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
+                        !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
+#if !CLIPMI_OLD_EPI
+  if constexpr (FAST && std::is_same<OutT, bf16>::value) {
+    if (stage && !p.ws && p.vec8) {
+      epilogue_lds_pipe<EPI < 0 ? 0 : EPI, AR, 2>(p, acc, mb, nb, lane, stage);
+      return;
+    }
+  }
+#endif
+  finish256<OutT, EPI, AR>(p, acc[0], mb, nb, lane, kz, stage);
+  finish256<OutT, EPI, AR>(p, acc[1], mb, nb + 64, lane, kz, stage);
 }
 
 // 4-wave 256x256 kernel (gemm4.hip) for the forward / dgrad layouts; nullptr if not covered
