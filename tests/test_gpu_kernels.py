@@ -137,6 +137,38 @@ def test_attention(dtype, B, N, H, causal, fa, monkeypatch):
         assert rel(dqkv[:, sl], g[:, sl]) < TOL[dtype] * 2, nm
 
 
+@pytest.mark.parametrize("B,N,H,causal", [(2, 197, 12, False), (90, 197, 12, False), (3, 150, 2, True),
+                                           (2, 224, 3, False), (2, 129, 2, False)])
+def test_attention_bwd_single_pass(B, N, H, causal, monkeypatch):
+    """The opt-in single-pass backward (attn_bwd_sp, CLIPMI_ATTN_BWD_SP=1: dQ from the dS^T image
+    instead of a second, recomputing phase) against the torch fp32 reference, like test_attention."""
+    monkeypatch.setenv("CLIPMI_ATTN_FA", "0")
+    monkeypatch.setenv("CLIPMI_ATTN_BWD_SP", "1")
+    dtype = torch.bfloat16
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 31, dtype)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(32)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    mp = mask.data_ptr() if mask is not None else None
+    o = torch.empty(B * N, D, dtype=dtype, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_attention_fwd", s, DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), mp, int(causal), B, H, N, D)
+    qr = qkv.float().requires_grad_(True)
+    oref, _ = attn_ref(qr, B, N, H, mask, causal)
+    do = rnd((B * N, D), 33, dtype)
+    oref.backward(do.float())
+    dqkv = torch.empty_like(qkv)
+    T.call("clipmi_attention_bwd", s, DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+           dqkv.data_ptr(), mp, int(causal), B, H, N, D)
+    for i, nm in enumerate("qkv"):
+        sl = slice(i * D, (i + 1) * D)
+        assert rel(dqkv[:, sl], qr.grad[:, sl]) < TOL[dtype] * 2, nm
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_text_embedding_fwd_bwd(dtype):
     B, S, D, V = 6, 77, 512, 1000

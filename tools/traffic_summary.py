@@ -7,14 +7,23 @@ Usage: traffic_summary.py FETCH_DIR WRITE_DIR OUT_PREFIX"""
 import csv, glob, json, os, sys
 
 FAMILIES = {
-    # wgrad: split-K gemm256 kernel; with CLIPMI_OVERLAP=0 each step's 97 launches come in program
-    # order, the vision backward's 48 encoder wgrads + the patch embedding first
-    "gemm256_wgrad": "gemm256_kernel<false, false, float, 0,",
+    # wgrad: split-K weight-gradient kernels (r02: gemm256_kernel; since r03 the persistent 4-wave
+    # gemm_w4p_kernel<false, false, float, ...>, demangled or mangled); with CLIPMI_OVERLAP=0 each
+    # step's 97 launches come in program order, the vision backward's 48 encoder wgrads + the patch
+    # embedding first
+    "gemm256_wgrad": ("gemm256_kernel<false, false, float, 0,", "gemm_w4p_kernel<false, false, float",
+                      "gemm_w4p_kernelILb0ELb0Ef"),
     # forward + dgrad: every gemm_pp_kernel instantiation; the vision tower's launches are the ones
     # whose grid is a multiple of its M tiles (B=1024: 201,728 rows = 788 tiles of 256)
-    "gemm256_fwd_dgrad": "gemm_pp_kernel",  # demangled or mangled names
+    "gemm256_fwd_dgrad": ("gemm_pp_kernel", "gemm_w4p_kernel<true", "gemm_w4p_kernelILb1"),  # demangled or mangled
 }
-PER_STEP, VISION, M_TILES = 97, 49, 788
+# r03 forward + dgrad launches per step in program order (CLIPMI_OVERLAP=0): text forward 48, the
+# patch embedding + vision forward 48, a 12-tile projection product, vision backward 48, an 8-tile
+# one, text backward 48 -- the vision tower's are positions 48 .. 145
+FD_PER_STEP, FD_VISION = 195, (48, 146)
+# r03: 99 wgrad launches per step -- a projection's (grid 6), the vision tower's 48 encoder wgrads +
+# the patch embedding, the text projection's (grid 4), the text tower's 48 (r02: 97, vision first)
+PER_STEP, VISION0, VISION, M_TILES = 99, 1, 49, 788
 WORKLOAD = "ViT-B/16/1024/1"  # bench.py's default run (config name / per-GPU batch / training), matched by bench.py
 
 
@@ -22,7 +31,8 @@ def per_dispatch(d, counter, kernel):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     out, grid = {}, {}
     for r in csv.DictReader(open(f)):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        pats = kernel if isinstance(kernel, tuple) else (kernel,)
+        if any(k in r["Kernel_Name"] for k in pats) and r["Counter_Name"] == counter:
             out[r["Dispatch_Id"]] = out.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
             grid[r["Dispatch_Id"]] = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
     ids = sorted(out, key=int)
@@ -32,8 +42,9 @@ def per_dispatch(d, counter, kernel):
 def vision_only(family, vals, grids):
     if family == "gemm256_wgrad":
         assert len(vals) % PER_STEP == 0, f"{len(vals)} wgrad launches is not a whole number of steps"
-        return [v for i, v in enumerate(vals) if i % PER_STEP < VISION]
-    return [v for v, g in zip(vals, grids) if g % M_TILES == 0]
+        return [v for i, v in enumerate(vals) if VISION0 <= i % PER_STEP < VISION0 + VISION]
+    assert len(vals) % FD_PER_STEP == 0, f"{len(vals)} forward/dgrad launches is not a whole number of steps"
+    return [v for i, v in enumerate(vals) if FD_VISION[0] <= i % FD_PER_STEP < FD_VISION[1]]
 
 
 def summarize(family, fetch_dir, write_dir):
@@ -53,6 +64,10 @@ def summarize(family, fetch_dir, write_dir):
 if __name__ == "__main__":
     # traffic_summary.py FETCH_DIR WRITE_DIR OUT_PREFIX  ->  OUT_PREFIX_wgrad.json, OUT_PREFIX_fwd_dgrad.json
     for fam, suffix in (("gemm256_wgrad", "wgrad"), ("gemm256_fwd_dgrad", "fwd_dgrad")):
-        res = summarize(fam, sys.argv[1], sys.argv[2])
+        try:
+            res = summarize(fam, sys.argv[1], sys.argv[2])
+        except (ZeroDivisionError, AssertionError) as e:  # r03: the K >= 1536 forward/dgrad launches are
+            print(fam, "not summarised:", e)               # persistent (grid 256), not matched by M tiles
+            continue
         json.dump(res, open(f"{sys.argv[3]}_{suffix}.json", "w"), indent=1)
         print(fam, json.dumps(res))

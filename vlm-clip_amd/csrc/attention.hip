@@ -1683,13 +1683,15 @@ int bwd_sp_dispatch(const AttnP& p, hipStream_t s) {
     default: return clipmi_invalid("attn_bwd_sp: N must be in (128, 224]");
   }
 }
-// the single-pass backward for 128 < N <= 224 unless CLIPMI_ATTN_BWD_SP=0 (A/B hook, read per
-// call).  (Its 4-wave form for the text tower, N = 77 with the causal mask, spilled at the 256
-// registers two workgroups per CU leave, so the text tower keeps attn_bwd_pf.)
+// the single-pass backward for 128 < N <= 224 with CLIPMI_ATTN_BWD_SP=1 (A/B hook, read per call).
+// Not the default: at ViT-B/16 (N = 197, B = 1024) it measured 912-976 us against attn_bwd_pf's
+// 889-926 (profiles/r03_attn_bwd_single_pass_ab.log): the per-step barrier and the dQ section's
+// dependent MFMA chain cost more than the recomputation they remove.  (Its 4-wave form for the
+// text tower, N = 77 with the causal mask, spilled at the 256 registers two workgroups per CU leave.)
 static bool use_bwd_sp(int N) {
   if (N <= 128 || N > 224) return false;
   const char* e = getenv("CLIPMI_ATTN_BWD_SP");
-  return !e || atoi(e) != 0;
+  return e && atoi(e) != 0;
 }
 
 // 4 waves per workgroup for N <= 128 (text: 5 blocks of 16 rows), else 8; each wave owns at

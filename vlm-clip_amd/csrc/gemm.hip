@@ -1267,7 +1267,9 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
   // production (var 0): the persistent 4-wave kernel for long-K products (K >= 1536), where its main
   // loop is 3-7 % faster than the ping-pong kernel's; at K = 768 / 512 the ping-pong kernel's 8 waves
   // run the VALU-heavy epilogues twice as fast per SIMD (tools/w4_stamps.py, profiles/r03_*)
-  const bool w4_default = p.var == 0 && p.K >= 1536;
+  // (and for fc2's input gradient with the stored-derivative product, K = 768: 1182 vs 1215 us,
+  // profiles/r03_gemm_dact_shapes.log)
+  const bool w4_default = p.var == 0 && (p.K >= 1536 || flags == E_MA);
   if ((w4_default || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || (p.var >= 28 && p.var <= 30)) &&
       !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
     GemmP q = p;

@@ -434,11 +434,22 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   }
 }
 
+// persistent grid: one workgroup per CU, or fewer with CLIPMI_W4P_GRID (A/B of leaving CUs to the
+// other tower's stream: a persistent launch holds its CUs until its last item; read once)
+int w4p_max_grid() {
+  static const int g = [] {
+    const char* e = getenv("CLIPMI_W4P_GRID");
+    const int c = num_cus_w4();
+    return (e && atoi(e) > 0) ? std::min(atoi(e), c) : c;
+  }();
+  return g;
+}
+
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
 void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
   (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>, L);
-  const int grid = std::min(p.ntiles * splits, num_cus_w4());
+  const int grid = std::min(p.ntiles * splits, w4p_max_grid());
   hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
 }
 
