@@ -15,6 +15,7 @@
 // column sums for biases, and LN backward with the residual gradient fused.
 // Activation buffers are caller-owned (per layer for training; one shared set for
 // inference), so the engine holds no state and allocates nothing.
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include "internal.h"
@@ -36,6 +37,25 @@ int clipmi_quant_mxfp8(void*, int, const void*, int64_t, int64_t, int, uint8_t*,
 
 namespace {
 
+// GEMM schedule override for the encoder being run (A/B of stream sharing): with
+// CLIPMI_TEXT_NONPERSIST=1 the causal (text) tower's GEMMs take the non-persistent 8-wave kernels
+// (forward/dgrad var 9, weight gradients var 4), whose workgroups free their CUs tile by tile, so
+// the vision tower's kernels on the other stream are not held behind a persistent launch
+thread_local int g_sched_fwd = 0, g_sched_wgrad = 0;
+struct SchedScope {
+  SchedScope(const clipmi_encoder_desc* d) {
+    static const bool on = [] {
+      const char* e = getenv("CLIPMI_TEXT_NONPERSIST");
+      return e && atoi(e) != 0;
+    }();
+    if (on && d->causal && d->dtype == CLIPMI_BF16) {
+      g_sched_fwd = 9;
+      g_sched_wgrad = 4;
+    }
+  }
+  ~SchedScope() { g_sched_fwd = g_sched_wgrad = 0; }
+};
+
 size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
@@ -54,6 +74,7 @@ int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool 
   d.ab_dtype = dt; d.c_dtype = c_dt; d.bias_dtype = dt;
   d.split_k = split; d.workspace = ws; d.workspace_bytes = ws_bytes;
   d.bias_grad = bias_grad;
+  if (dt == CLIPMI_BF16) d.force_small_tile = (!akm && !bkm) ? g_sched_wgrad : g_sched_fwd;
   return clipmi_gemm(s, &d);
 }
 
@@ -173,6 +194,7 @@ extern "C" int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d) { return 
 
 extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
   CLIPMI_TRY(validate(d));
+  SchedScope sched(d);
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
@@ -235,6 +257,7 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
 // Layers layer_hi-1 down to layer_lo only: the data-parallel path calls the backward in chunks and
 // all-reduces each chunk's (contiguous) gradient slice while the next chunk computes.
 extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo) {
+  SchedScope sched(d);
   CLIPMI_TRY(validate(d));
   CLIPMI_REQUIRE(d->dtype != CLIPMI_FP8, "the fp8 encoder is forward-only (frozen towers)");
   CLIPMI_REQUIRE(0 <= layer_lo && layer_lo <= layer_hi && layer_hi <= d->L, "layer range");
