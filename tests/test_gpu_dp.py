@@ -1,5 +1,5 @@
-"""Data-parallel path with the real kernels: 2 ranks share cuda:0 over a gloo group
-(RCCL needs one GPU per rank; the driver's 8-GPU run exercises RCCL itself).  The sum of
+"""Data-parallel path with the real kernels: 2 ranks share cuda:0 over a gloo group, and, where
+two GPUs are visible, 2 ranks over RCCL (one GPU each; skipped on a one-GPU box).  The sum of
 the ranks' losses and the all-reduced gradients must equal the single-device result on
 the same global batch, fp32 parity mode."""
 import os
@@ -13,16 +13,16 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False):
+def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False, backend="gloo"):
     try:
-        _worker_body(rank, world, port, q, overlap, chunk, shared)
+        _worker_body(rank, world, port, q, overlap, chunk, shared, backend)
     except BaseException:  # report instead of leaving the parent waiting on the queue
         import traceback
         q.put((rank, None, traceback.format_exc()))
         raise
 
 
-def _worker_body(rank, world, port, q, overlap, chunk, shared):
+def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo"):
     import sys
     if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
         os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
@@ -32,16 +32,19 @@ def _worker_body(rank, world, port, q, overlap, chunk, shared):
     from clipmi.trainer import FusedAdamW
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo: both ranks on cuda:0; nccl (= RCCL): one GPU per rank, the backend production uses
+    dev = f"cuda:{rank}" if backend == "nccl" else "cuda:0"
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     # shared adapters need text hidden 512 (their text_projection, model_m.py:54-61): B/32
     m = CLIPWithAdapters("B/32" if shared else "tiny", use_text_adapter=True, use_vision_adapter=True,
                          use_shared_adapters=shared,
-                         freeze_clip=False, device="cuda:0", precision="fp32", pooling="eos",
+                         freeze_clip=False, device=dev, precision="fp32", pooling="eos",
                          process_group=dist.group.WORLD)
     if shared:
         m.eval()  # shared-adapter dropout off: the ranks must reproduce the single-device gradients
     B = 4
-    b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
+    b = {k: torch.from_numpy(v).to(dev) for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
     if overlap:  # gradient buckets all-reduced from the towers' chunked backward (GradBucketReducer)
         opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas(),
                          process_group=dist.group.WORLD).overlap_with(m)
@@ -58,18 +61,24 @@ def _worker_body(rank, world, port, q, overlap, chunk, shared):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,chunk,shared", [(False, None, False), (True, None, False), (False, 3, False),
-                                                  (True, None, True)])
-def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared):
+@pytest.mark.parametrize("overlap,chunk,shared,backend", [(False, None, False, "gloo"), (True, None, False, "gloo"),
+                                                          (False, 3, False, "gloo"), (True, None, True, "gloo"),
+                                                          # RCCL, one GPU per rank: the comm-stream ordering the
+                                                          # overlapped reducer relies on
+                                                          (True, None, False, "nccl"), (False, 3, False, "nccl")])
+def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared, backend):
     """shared=True: shared adapters on an unfrozen CLIP add a position-embedding gradient after the
-    vision tower's backward, so the overlapped reducer must leave that block to finish()."""
+    vision tower's backward, so the overlapped reducer must leave that block to finish().
+    backend nccl needs two visible GPUs (skipped on a one-GPU box)."""
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL ranks need one GPU each")
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500
-    port += 37 * int(overlap) + 71 * int(chunk is not None) + 113 * int(shared)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk, shared)) for r in range(2)]
+    port += 37 * int(overlap) + 71 * int(chunk is not None) + 113 * int(shared) + 157 * int(backend == "nccl")
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk, shared, backend)) for r in range(2)]
     for p in procs:
         p.start()
     res = []

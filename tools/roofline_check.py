@@ -10,8 +10,11 @@ for r in rows:
     if "attn_fwd_pf<14" in r["Kernel_Name"]:
         main = r["Stream_Id"]
         break
-FAMILIES = {"gemm256_wgrad": ("gemm256_kernel<false, false, float, 0,", "gemm256_kernelILb0ELb0EfLi0E"),
-            "gemm256_fwd_dgrad": ("gemm_pp_kernel",)}
+# r03: the persistent 4-wave kernel carries the weight gradients and the K >= 1536 forward/dgrad
+# products (plus fc2's input gradient), demangled or mangled names
+FAMILIES = {"gemm256_wgrad": ("gemm256_kernel<false, false, float, 0,", "gemm256_kernelILb0ELb0EfLi0E",
+                              "gemm_w4p_kernel<false, false, float", "gemm_w4p_kernelILb0ELb0Ef"),
+            "gemm256_fwd_dgrad": ("gemm_pp_kernel", "gemm_w4p_kernel<true", "gemm_w4p_kernelILb1")}
 for fam, pats in FAMILIES.items():
     dur = defaultdict(list)
     for r in rows:
