@@ -226,9 +226,10 @@ def _take(kind, t, idx):
 def test_b16_full_finetune_gradients_fp32(golden):
     """BASELINE config 3's workload (ViT-B/16 full fine-tune, adapters off, logit_scale trainable)
     at B=2 in the fp32 parity mode: every parameter's gradient (sampled rows) vs the reference's
-    loss backward within 2e-3 of the tensor's scale (floored at 5 % of the largest gradient:
+    loss backward within 1e-3 of the tensor's scale (floored at 5 % of the largest gradient:
     k-projection biases and text q/k are exactly zero in the reference, quirk Q1).  Measured
-    1.0-1.3e-3 on logit_scale and the vision embeddings.  That is this fixture's conditioning, not
+    7.9e-4 (r03; 1.0-1.3e-3 in r02, before fc1 stored quick_gelu' from the fp32 pre-activation) on
+    the vision embeddings and logit_scale.  That is this fixture's conditioning, not
     a kernel error (numbers: test_oracle_golden.test_b16_contrastive_b2_is_ill_conditioned): the two
     text rows are identical (Q1), the logits [[5.20, 5.24]] x 2, and a 1e-6 relative perturbation of
     the reference's own features moves the image-feature gradient by ~5e-4 of its scale in fp64
@@ -254,7 +255,7 @@ def test_b16_full_finetune_gradients_fp32(golden):
     errs.sort(reverse=True)
     worst = errs[0]
     print(f"\n[b16 full fp32] largest grad errs {[(round(e, 6), n) for e, n in errs[:6]]}")
-    assert worst[0] < 2e-3, worst
+    assert worst[0] < 1e-3, worst
 
 
 def test_b16_feature_gradients_fp32(golden):
@@ -360,7 +361,7 @@ def test_b32_adapter_b256_matches_reference(golden, precision):
         # bf16 logits (within 0.15 at scale 100) move individual softmax weights by a few percent,
         # so elementwise bounds measure the softmax's conditioning; the gradient's direction is
         # what the bf16 arithmetic must preserve
-        assert worst_cos[0] > 0.99, worst_cos
+        assert worst_cos[0] > 0.993, worst_cos  # measured 0.9951 (r03)
 
 
 def test_shared_adapters_unfrozen_position_embedding_grad(golden):
@@ -448,9 +449,9 @@ def test_shared_adapters_training_dropout_matches_oracle_with_same_masks():
 # mantissa bits, one power-of-two scale per 32 inputs), i.e. ~2-3 % per element, over 24 + 12
 # layers; the logits (100 x cosine) are bounded by FP8_LOGIT_TOL and the features' direction by a
 # cosine similarity with the reference's.
-# Bounds ~2x the measured error (L/14@336 B=2: 0.23-0.28; B/32 B=8: 0.82 -- its 512-wide
-# features and 12-layer towers round more per logit than L/14's 768-wide ones).
-FP8_LOGIT_TOL = {"l14_336": 0.5, "b32": 1.6}
+# Bounds ~2x the measured error (r03: L/14@336 B=2 0.234, B/32 B=8 0.243; bf16 on the same
+# fixtures 0.10 / 0.07).
+FP8_LOGIT_TOL = {"l14_336": 0.5, "b32": 0.5}
 FP8_FEATURE_COS = 0.99
 
 
@@ -636,3 +637,26 @@ def test_config3_full_size_overlap_is_bitwise_serial(monkeypatch):
     racy = [n for n in g0 if not torch.equal(g0[n], g1[n]) and not any(k in n for k in _ATOMIC_GRADS)]
     print(f"\n[config 3 full size] loss {l0.item():.5f}; {len(g0)} gradients, differing beyond atomics: {racy[:6]}")
     assert not racy
+
+
+@pytest.mark.parametrize("B", [64])
+def test_b16_full_bf16_forward_batch64_matches_oracle(B):
+    """Config 3's model (ViT-B/16, full fine-tune setup, bf16 MFMA path) at a wider batch than the
+    B <= 8 goldens: the [B, B] contrastive logits and loss against the CPU oracle (oracle/clip_ref.py,
+    pinned to the reference by forward_b16.npz) in fp32 on the same synthetic weights and batch.
+    Stated bf16 bound as for the goldens: 0.15 at logit scale 100."""
+    from oracle import clip_ref as R
+    torch.set_num_threads(16)
+    m = make("B/16", False, "bf16", freeze=False)
+    b = batch(m.config, B, seed=777)
+    with torch.no_grad():
+        out = m(**b)
+    torch.cuda.synchronize()
+    p = R.to_torch(synth.clip_state_dict(m.config, seed=0))
+    with torch.no_grad():
+        ref = R.clip_with_adapters_forward({k: x.cpu() for k, x in b.items()}, p, m.config)
+    err = float((out["logits_per_text"].float().cpu() - ref["logits_per_text"]).abs().max())
+    lerr = abs(out["loss"].item() - ref["loss"].item())
+    print(f"\n[b16 bf16 B={B}] max|dlogit| {err:.4f}, |dloss| {lerr:.2e}")
+    assert err < LOGIT_TOL["bf16"], err
+    assert lerr < 0.02, lerr
