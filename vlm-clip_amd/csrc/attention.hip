@@ -1108,8 +1108,37 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_sp(AttnP p, int nite
 #pragma unroll
       for (int v = 0; v < 4; ++v) { dv[u][v] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u][v] = dv[u][v]; }
 
+    // dQ^T of step sq (dS^T in half sq & 1): this wave's tile(s) over all keys (causal: keys <= the
+    // step's last query).  Run one step late, before the next step's phase A, so its dependent MFMA
+    // chain and LDS reads overlap that phase's independent work instead of idling after a barrier.
+    auto dq_step = [&](int sq) {
+      const int hq = sq & 1;
+      const int kcl = CAUSAL ? min(NKC, sq + 1) : NKC;
+#pragma unroll
+      for (int j = 0; j < NQT; ++j) {
+        const int qt = NQT == 1 ? (wave >> 2) : j;
+        f32x4 acc2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          if (kc < kcl) {
+            const bf16x8 kt = frag_tr(Kimg, kc * 32, dt * 16, lane);
+            const bf16x8 st = frag_tr(dSimg, kc * 32, hq * 32 + qt * 16, lane);
+            acc2[kc & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, st, acc2[kc & 1], 0, 0, 0);
+          }
+        }
+        const f32x4 acc = acc2[0] + acc2[1];
+        const int q = sq * 32 + qt * 16 + li;
+        if (q < N) {
+          float a[4] = {acc[0] * p.scale, acc[1] * p.scale, acc[2] * p.scale, acc[3] * p.scale};
+          store4(dq_base + (int64_t)q * ld + dt * 16 + 4 * g, a);
+        }
+      }
+    };
     for (int qs = 0; qs < nstep; ++qs) {
       const int hb = qs & 1;
+      // half hb^1 holds dS(qs - 1), made visible by the previous barrier; half hb's last reader
+      // (dQ(qs - 2)) ran before that barrier, so this step may overwrite it
+      if (qs > 0) dq_step(qs - 1);
       bool act[NB];
 #pragma unroll
       for (int u = 0; u < NB; ++u) act[u] = kbv[u] && !(CAUSAL && qs * 32 + 31 < (wave + NW * u) * 16);
@@ -1170,29 +1199,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_sp(AttnP p, int nite
       }
       raw_barrier_lds();  // dS(qs) complete; every wave done with step qs's Q / dO rows
       if (more) issue_qdo(nxt, qs * 4, qs * 4 + 4);
-      // dQ^T of step qs: this wave's tile(s) over all keys (causal: keys <= the step's last query)
-      const int kcl = CAUSAL ? min(NKC, qs + 1) : NKC;
-#pragma unroll
-      for (int j = 0; j < NQT; ++j) {
-        const int qt = NQT == 1 ? (wave >> 2) : j;
-        // two independent accumulation chains (even / odd key chunks): half the dependent MFMA latency
-        f32x4 acc2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
-          if (kc < kcl) {
-            const bf16x8 kt = frag_tr(Kimg, kc * 32, dt * 16, lane);
-            const bf16x8 st = frag_tr(dSimg, kc * 32, hb * 32 + qt * 16, lane);
-            acc2[kc & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, st, acc2[kc & 1], 0, 0, 0);
-          }
-        }
-        const f32x4 acc = acc2[0] + acc2[1];
-        const int q = qs * 32 + qt * 16 + li;
-        if (q < N) {
-          float a[4] = {acc[0] * p.scale, acc[1] * p.scale, acc[2] * p.scale, acc[3] * p.scale};
-          store4(dq_base + (int64_t)q * ld + dt * 16 + 4 * g, a);
-        }
-      }
     }
+    dq_step(nstep - 1);  // the last step's dS^T, visible after its barrier
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       if (kbv[u] && key[u] < N) {
@@ -1685,8 +1693,8 @@ int bwd_sp_dispatch(const AttnP& p, hipStream_t s) {
 }
 // the single-pass backward for 128 < N <= 224 with CLIPMI_ATTN_BWD_SP=1 (A/B hook, read per call).
 // Not the default: at ViT-B/16 (N = 197, B = 1024) it measured 912-976 us against attn_bwd_pf's
-// 889-926 (profiles/r03_attn_bwd_single_pass_ab.log): the per-step barrier and the dQ section's
-// dependent MFMA chain cost more than the recomputation they remove.  (Its 4-wave form for the
+// 889-926, and 938-981 vs 884-896 with dQ one step late (profiles/r03_attn_bwd_single_pass_ab.log):
+// the per-step barrier and the dQ reads cost more than the recomputation they remove.  (Its 4-wave form for the
 // text tower, N = 77 with the causal mask, spilled at the 256 registers two workgroups per CU leave.)
 static bool use_bwd_sp(int N) {
   if (N <= 128 || N > 224) return false;
