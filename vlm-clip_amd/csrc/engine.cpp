@@ -20,6 +20,7 @@
 #include <cstring>
 #include "internal.h"
 #include <atomic>
+#include <mutex>
 
 extern "C" {
 int clipmi_layernorm_fwd(void*, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int, int,
@@ -55,6 +56,45 @@ struct SchedScope {
   }
   ~SchedScope() { g_sched_fwd = g_sched_wgrad = 0; }
 };
+
+// Deferred split-K reduces (A/B, CLIPMI_DEFER_REDUCE=1, bf16): a weight-gradient GEMM's slab reduce
+// runs on a per-device side stream after an event, so the tower's stream goes on to its next kernel
+// instead of waiting for CUs for a small reduce; the slabs rotate over NSLOT workspace slots (a slot
+// is reused only after its reduce's event), and each backward call ends by joining the side stream.
+constexpr int NSLOT = 8;
+bool defer_reduce() {
+  static const bool on = [] {
+    const char* e = getenv("CLIPMI_DEFER_REDUCE");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+struct DeferCtx {
+  hipStream_t side = nullptr;
+  hipEvent_t after[NSLOT], done[NSLOT], join;
+  bool used[NSLOT] = {};
+  int next = 0;
+};
+DeferCtx* defer_ctx() {
+  static std::mutex mu;
+  static DeferCtx* ctx[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  dev &= 63;
+  std::lock_guard<std::mutex> g(mu);
+  if (!ctx[dev]) {
+    DeferCtx* c = new DeferCtx();
+    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (int i = 0; i < NSLOT; ++i) {
+      if (hipEventCreateWithFlags(&c->after[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    }
+    if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return nullptr;
+    ctx[dev] = c;
+  }
+  return ctx[dev];
+}
 
 size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -146,6 +186,7 @@ WsPlan plan(const clipmi_encoder_desc* d) {
     const int s = wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
     if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * (sh[1] + 1) * 4);  // slabs + bias partials
   }
+  if (defer_reduce() && d->dtype == CLIPMI_BF16) sp = align256(sp) * NSLOT;  // rotating slab slots
   p.colsum = p.split + align256(sp);
   p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));
   p.total = p.ln + align256(clipmi_layernorm_bwd_ws((int)R, d->D));
@@ -278,12 +319,26 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   const int64_t col_bytes = p.ln - p.colsum;
   const int64_t ln_bytes = p.total - p.ln;
   const int f32 = CLIPMI_F32;
+  DeferCtx* dctx = (defer_reduce() && dt == CLIPMI_BF16) ? defer_ctx() : nullptr;
   // wgrad: C[M,N] += sum_tokens A[t][m] B[t][n]; the bf16 path also fuses the Linear bias
   // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
   auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                    float* bgrad) -> int {
     const int sp = wgrad_splits(M, N, R, dt);
     const bool fuse = dt == CLIPMI_BF16;
+    if (dctx && sp > 1) {  // deferred slab reduce: next slot, its previous reduce retired first
+      const int slot = dctx->next++ % NSLOT;
+      if (dctx->used[slot]) CLIPMI_HIP(hipStreamWaitEvent((hipStream_t)s, dctx->done[slot], 0));
+      const int64_t sb = split_bytes / NSLOT & ~(int64_t)255;
+      gemm_set_reduce_stream(dctx->side, dctx->after[slot]);
+      const int st = gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
+                          nullptr, 0, sp, (char*)wsplit + slot * sb, sb, bgrad);
+      gemm_set_reduce_stream(nullptr, nullptr);
+      CLIPMI_TRY(st);
+      CLIPMI_HIP(hipEventRecord(dctx->done[slot], dctx->side));
+      dctx->used[slot] = true;
+      return CLIPMI_OK;
+    }
     CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
                     nullptr, 0, sp, wsplit, split_bytes, fuse ? bgrad : nullptr));
     if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
@@ -311,6 +366,10 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
     CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
                                     g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
+  }
+  if (dctx) {  // every deferred reduce of this call lands before the caller's next work on s
+    CLIPMI_HIP(hipEventRecord(dctx->join, dctx->side));
+    CLIPMI_HIP(hipStreamWaitEvent((hipStream_t)s, dctx->join, 0));
   }
   return CLIPMI_OK;
 }

@@ -1374,6 +1374,13 @@ extern "C" int clipmi_gemm_stamps(void* buf) {
   return CLIPMI_OK;
 }
 
+static thread_local hipStream_t g_reduce_stream = nullptr;
+static thread_local hipEvent_t g_after_gemm = nullptr;
+void gemm_set_reduce_stream(hipStream_t rs, hipEvent_t after_gemm) {
+  g_reduce_stream = rs;
+  g_after_gemm = after_gemm;
+}
+
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
@@ -1530,6 +1537,11 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }
   CLIPMI_CHECK_LAUNCH();
   if (p.ws) {
+    if (g_reduce_stream && g_after_gemm) {  // the slab reduce on the engine's side stream
+      CLIPMI_HIP(hipEventRecord(g_after_gemm, s));
+      CLIPMI_HIP(hipStreamWaitEvent(g_reduce_stream, g_after_gemm, 0));
+      s = g_reduce_stream;
+    }
     const int64_t total = (int64_t)d->M * d->N;
     const int beta = (d->flags & CLIPMI_EPI_BETA) ? 1 : 0;
     if (d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0 && ((uintptr_t)p.ws & 15) == 0) {
