@@ -55,7 +55,7 @@ for name, B, N, H, causal in SHAPES:
                 fl = 4.0 * B * H * N * npad * 64
                 print(f"{name:16s} nw{nw:>2s} fwd {kern}: {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
             os.environ["CLIPMI_ATTN_FA"] = "0"
-            for sp in os.environ.get("ATTN_BWD_SP", "1").split(","):  # single-pass backward A/B
+            for sp in os.environ.get("ATTN_BWD_SP", "0").split(","):  # 0: production two-phase; 1: single-pass (A/B)
                 os.environ["CLIPMI_ATTN_BWD_SP"] = sp
                 ms = timeit(bwd)
                 fl = 10.0 * B * H * N * npad * 64
