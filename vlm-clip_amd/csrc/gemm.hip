@@ -1447,6 +1447,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }
   int splits = d->split_k > 1 ? d->split_k : 1;
   GemmP p;
+  memset(&p, 0, sizeof(p));
   p.M = d->M; p.N = d->N; p.K = d->K;
   p.A = d->A; p.lda = d->lda; p.B = d->B; p.ldb = d->ldb;
   p.C = d->C; p.ldc = d->ldc; p.bias = d->bias; p.res = d->residual; p.ldr = d->ldr;

@@ -31,6 +31,8 @@
 //    per A fragment against a ones fragment (waves wn == 0 of n-tile 0), per-split partials summed
 //    in split order afterwards (deterministic).
 #include "gemm_common.h"
+#include <mutex>
+#include <vector>
 
 namespace cmg {
 namespace {
@@ -383,9 +385,16 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   const bf16x8 ones = w4_ones();
   const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
+  // dynamic queue (p.dyn): after its first item (the static XCD-aware one) a workgroup takes the next
+  // unclaimed item from a counter, so a workgroup that started late -- its CU held by the other
+  // tower's stream -- takes fewer items instead of stretching the launch's tail.  Lane 0 of wave 0
+  // claims the next item at the start of the current one (a vector atomic: divergent lane), and the
+  // value reaches the other waves through LDS between two barriers after the main loop.
+  int claimed = 0;
   while (true) {
     int m0, n0, kz, kbeg, kend;
     coords(item, m0, n0, kz, kbeg, kend);
+    if (p.dyn && t == 0) claimed = atomicAdd(p.dyn, 1) + nwg;
     const int ns = (kend - kbeg + 63) / 64;
     const bool bias_wave = BG && n0 == 0 && wn == 0;
 #pragma unroll
@@ -413,7 +422,18 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
       w4_half<AK, BKM, true, true, BG>(acc, accb, bias_wave, ones, a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb, lda, ldb);
     }
     w4_mfma_drain();
-    const int next = item + nwg;
+    int next = item + nwg;
+    if (p.dyn) {  // broadcast the claimed item through the (idle) first stage, then free it again
+      // (vmcnt(0) first: the last step's empty-descriptor DMAs may still be writing zeros into a
+      // stage, and wave 0's first piece covers byte 0)
+      __builtin_amdgcn_s_waitcnt(0x0f70);
+      if (t == 0) *LDS_PTR(int, smem) = claimed;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      next = __builtin_amdgcn_readfirstlane(*LDS_PTR(const int, smem));
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
     // every wave's last useful stage read came before the last step's barrier (the final
     // half-step's reads fetch fragments nobody uses), so the next item may overwrite both stages
     if (next < nitems) prologue_dma(next);
@@ -432,10 +452,39 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
     if (next >= nitems) break;
     item = next;
   }
+  if (p.dyn && t == 0) {  // the last workgroup out resets both counters for the stream's next launch
+    __threadfence();
+    if (atomicAdd(p.dyn + 1, 1) == nwg - 1) {
+      atomicExch(p.dyn, 0);
+      atomicExch(p.dyn + 1, 0);
+    }
+  }
 }
 
 // persistent grid: one workgroup per CU, or fewer with CLIPMI_W4P_GRID (A/B of leaving CUs to the
 // other tower's stream: a persistent launch holds its CUs until its last item; read once)
+// dynamic-queue counters (CLIPMI_W4P_DYN=1, read once): one pair per stream, zeroed at allocation and
+// re-zeroed by each launch's last workgroup; launches on one stream are ordered, so they never overlap
+int* w4p_dyn_counters(hipStream_t s) {
+  static const bool on = [] {
+    const char* e = getenv("CLIPMI_W4P_DYN");
+    return e && atoi(e) != 0;
+  }();
+  if (!on) return nullptr;
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, hipStream_t>, int*>> tab;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : tab)
+    if (e.first.first == dev && e.first.second == s) return e.second;
+  int* c = nullptr;
+  if (hipMalloc(&c, 2 * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(c, 0, 2 * sizeof(int)) != hipSuccess) return nullptr;
+  tab.push_back({{dev, s}, c});
+  return c;
+}
+
 int w4p_max_grid() {
   static const int g = [] {
     const char* e = getenv("CLIPMI_W4P_GRID");
@@ -450,7 +499,9 @@ void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
   (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>, L);
   const int grid = std::min(p.ntiles * splits, w4p_max_grid());
-  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
+  GemmP q = p;
+  q.dyn = w4p_dyn_counters(s);
+  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>), dim3(grid), dim3(W4_THR), L, s, q, bias_grad);
 }
 
 template <bool BKM, int EPI>

@@ -31,6 +31,7 @@ struct GemmP {
   int raster;  // 0: tiles row-major; g > 0: g tile-rows at a time, column by column (tile_coords)
   float* bws;  // split-K with a fused bias gradient: per-split partial sums [splits][M] (no atomics)
   unsigned long long* dbg;  // diagnostic builds only: in-kernel s_memtime stamps (clipmi_gemm_stamps)
+  int* dyn;  // persistent 4-wave kernel: {next-item counter, finished-workgroup counter} (dynamic queue) or null
 };
 
 // host side: the stamp buffer armed by clipmi_gemm_stamps (nullptr when disarmed)
