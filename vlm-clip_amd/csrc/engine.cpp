@@ -78,20 +78,29 @@ struct DeferCtx {
 DeferCtx* defer_ctx() {
   static std::mutex mu;
   static DeferCtx* ctx[64] = {};
+  static bool failed[64] = {};  // creation failed once on this device: run undeferred, do not retry
   int dev = 0;
   (void)hipGetDevice(&dev);
   dev &= 63;
   std::lock_guard<std::mutex> g(mu);
-  if (!ctx[dev]) {
-    DeferCtx* c = new DeferCtx();
-    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    for (int i = 0; i < NSLOT; ++i) {
-      if (hipEventCreateWithFlags(&c->after[i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess)
-        return nullptr;
+  if (!ctx[dev] && !failed[dev]) {
+    DeferCtx c;
+    bool ok = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) == hipSuccess;
+    int ne = 0;  // events created so far, in order after[0], done[0], after[1], ...
+    for (int i = 0; ok && i < NSLOT; ++i) {
+      ok = hipEventCreateWithFlags(&c.after[i], hipEventDisableTiming) == hipSuccess;
+      ne += ok;
+      ok = ok && hipEventCreateWithFlags(&c.done[i], hipEventDisableTiming) == hipSuccess;
+      ne += ok;
     }
-    if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    ctx[dev] = c;
+    bool joined = ok && hipEventCreateWithFlags(&c.join, hipEventDisableTiming) == hipSuccess;
+    if (!joined) {  // release what was created
+      for (int j = 0; j < ne; ++j) (void)hipEventDestroy(j & 1 ? c.done[j >> 1] : c.after[j >> 1]);
+      if (c.side) (void)hipStreamDestroy(c.side);
+      failed[dev] = true;
+      return nullptr;
+    }
+    ctx[dev] = new DeferCtx(c);
   }
   return ctx[dev];
 }
