@@ -54,6 +54,56 @@ def test_invalid_args_raise_without_gpu():
         _lib.check(st, "clipmi_gemm")
 
 
+def _gemm_desc(flags, **ptrs):
+    from clipmi._lib import GemmDesc
+    d = GemmDesc()
+    d.M, d.N, d.K = 256, 256, 64
+    d.ab_dtype = d.c_dtype = 1
+    d.A, d.B, d.C = 4096, 8192, 12288  # never dereferenced: validation rejects before any launch
+    d.lda = d.ldb = 64
+    d.ldc = d.ldr = d.ldaux = 256
+    d.alpha = 1.0
+    d.flags = flags
+    for k, v in ptrs.items():
+        setattr(d, k, v)
+    return d
+
+
+@pytest.mark.parametrize("flag,operand", [
+    ("EPI_DQGELU", "aux"), ("EPI_DGELU", "aux"), ("EPI_MUL_AUX", "aux"), ("EPI_STORE_PRE", "aux"),
+    ("EPI_STORE_DACT", "aux"), ("EPI_RESID", "residual"), ("EPI_BIAS", "bias")])
+def test_epilogue_flag_without_operand_is_rejected(flag, operand):
+    """Every epilogue flag that reads or writes an operand returns CLIPMI_ERR_INVALID when that
+    operand is missing, before any launch: a null aux with an aux-reading epilogue once faulted a
+    GPU in a bench tool (csrc/gemm.hip clipmi_gemm validation)."""
+    import ctypes
+    from clipmi import _lib
+    f = getattr(_lib, flag)
+    if flag == "EPI_STORE_DACT":
+        f |= _lib.EPI_QGELU
+    ptrs = {"aux": 16384, "residual": 20480, "bias": 24576}
+    ptrs[operand] = None
+    d = _gemm_desc(f, **ptrs)
+    st = _lib.lib().clipmi_gemm(None, ctypes.byref(d))
+    assert st == -1, (flag, st)
+    assert operand.encode()[:3] in _lib.lib().clipmi_last_error()
+
+
+@pytest.mark.parametrize("combo", [("EPI_STORE_PRE", "EPI_STORE_DACT"), ("EPI_MUL_AUX", "EPI_RESID"),
+                                   ("EPI_MUL_AUX", "EPI_BETA"), ("EPI_DQGELU", "EPI_STORE_PRE"),
+                                   ("EPI_MUL_AUX", "EPI_DQGELU")])
+def test_epilogue_flag_conflicts_are_rejected(combo):
+    """Flag pairs that would give aux two roles, or feed one epilogue input stream to two
+    operations, are rejected on the host (the kernels' static_asserts cover the compiled forms)."""
+    import ctypes
+    from clipmi import _lib
+    f = _lib.EPI_QGELU
+    for c in combo:
+        f |= getattr(_lib, c)
+    d = _gemm_desc(f, aux=16384, residual=20480, bias=24576)
+    assert _lib.lib().clipmi_gemm(None, ctypes.byref(d)) == -1
+
+
 def test_param_names_match_hf_clipmodel():
     from transformers import CLIPConfig, CLIPModel
     from clipmi.modules import CLIPParams

@@ -20,7 +20,6 @@
 #include <cstring>
 #include "internal.h"
 #include <atomic>
-#include <mutex>
 
 extern "C" {
 int clipmi_layernorm_fwd(void*, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int, int,
@@ -37,73 +36,6 @@ int clipmi_quant_mxfp8(void*, int, const void*, int64_t, int64_t, int, uint8_t*,
 }
 
 namespace {
-
-// GEMM schedule override for the encoder being run (A/B of stream sharing): with
-// CLIPMI_TEXT_NONPERSIST=1 the causal (text) tower's GEMMs take the non-persistent 8-wave kernels
-// (forward/dgrad var 9, weight gradients var 4), whose workgroups free their CUs tile by tile, so
-// the vision tower's kernels on the other stream are not held behind a persistent launch
-thread_local int g_sched_fwd = 0, g_sched_wgrad = 0;
-struct SchedScope {
-  SchedScope(const clipmi_encoder_desc* d) {
-    static const bool on = [] {
-      const char* e = getenv("CLIPMI_TEXT_NONPERSIST");
-      return e && atoi(e) != 0;
-    }();
-    if (on && d->causal && d->dtype == CLIPMI_BF16) {
-      g_sched_fwd = 9;
-      g_sched_wgrad = 4;
-    }
-  }
-  ~SchedScope() { g_sched_fwd = g_sched_wgrad = 0; }
-};
-
-// Deferred split-K reduces (A/B, CLIPMI_DEFER_REDUCE=1, bf16): a weight-gradient GEMM's slab reduce
-// runs on a per-device side stream after an event, so the tower's stream goes on to its next kernel
-// instead of waiting for CUs for a small reduce; the slabs rotate over NSLOT workspace slots (a slot
-// is reused only after its reduce's event), and each backward call ends by joining the side stream.
-constexpr int NSLOT = 8;
-bool defer_reduce() {
-  static const bool on = [] {
-    const char* e = getenv("CLIPMI_DEFER_REDUCE");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-struct DeferCtx {
-  hipStream_t side = nullptr;
-  hipEvent_t after[NSLOT], done[NSLOT], join;
-  bool used[NSLOT] = {};
-  int next = 0;
-};
-DeferCtx* defer_ctx() {
-  static std::mutex mu;
-  static DeferCtx* ctx[64] = {};
-  static bool failed[64] = {};  // creation failed once on this device: run undeferred, do not retry
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  dev &= 63;
-  std::lock_guard<std::mutex> g(mu);
-  if (!ctx[dev] && !failed[dev]) {
-    DeferCtx c;
-    bool ok = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) == hipSuccess;
-    int ne = 0;  // events created so far, in order after[0], done[0], after[1], ...
-    for (int i = 0; ok && i < NSLOT; ++i) {
-      ok = hipEventCreateWithFlags(&c.after[i], hipEventDisableTiming) == hipSuccess;
-      ne += ok;
-      ok = ok && hipEventCreateWithFlags(&c.done[i], hipEventDisableTiming) == hipSuccess;
-      ne += ok;
-    }
-    bool joined = ok && hipEventCreateWithFlags(&c.join, hipEventDisableTiming) == hipSuccess;
-    if (!joined) {  // release what was created
-      for (int j = 0; j < ne; ++j) (void)hipEventDestroy(j & 1 ? c.done[j >> 1] : c.after[j >> 1]);
-      if (c.side) (void)hipStreamDestroy(c.side);
-      failed[dev] = true;
-      return nullptr;
-    }
-    ctx[dev] = new DeferCtx(c);
-  }
-  return ctx[dev];
-}
 
 size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -123,7 +55,6 @@ int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool 
   d.ab_dtype = dt; d.c_dtype = c_dt; d.bias_dtype = dt;
   d.split_k = split; d.workspace = ws; d.workspace_bytes = ws_bytes;
   d.bias_grad = bias_grad;
-  if (dt == CLIPMI_BF16) d.force_small_tile = (!akm && !bkm) ? g_sched_wgrad : g_sched_fwd;
   return clipmi_gemm(s, &d);
 }
 
@@ -195,7 +126,6 @@ WsPlan plan(const clipmi_encoder_desc* d) {
     const int s = wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
     if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * (sh[1] + 1) * 4);  // slabs + bias partials
   }
-  if (defer_reduce() && d->dtype == CLIPMI_BF16) sp = align256(sp) * NSLOT;  // rotating slab slots
   p.colsum = p.split + align256(sp);
   p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));
   p.total = p.ln + align256(clipmi_layernorm_bwd_ws((int)R, d->D));
@@ -244,7 +174,6 @@ extern "C" int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d) { return 
 
 extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
   CLIPMI_TRY(validate(d));
-  SchedScope sched(d);
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
@@ -307,7 +236,6 @@ extern "C" int clipmi_encoder_bwd(void* s, const clipmi_encoder_desc* d, void* d
 // Layers layer_hi-1 down to layer_lo only: the data-parallel path calls the backward in chunks and
 // all-reduces each chunk's (contiguous) gradient slice while the next chunk computes.
 extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo) {
-  SchedScope sched(d);
   CLIPMI_TRY(validate(d));
   CLIPMI_REQUIRE(d->dtype != CLIPMI_FP8, "the fp8 encoder is forward-only (frozen towers)");
   CLIPMI_REQUIRE(0 <= layer_lo && layer_lo <= layer_hi && layer_hi <= d->L, "layer range");
@@ -328,26 +256,12 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   const int64_t col_bytes = p.ln - p.colsum;
   const int64_t ln_bytes = p.total - p.ln;
   const int f32 = CLIPMI_F32;
-  DeferCtx* dctx = (defer_reduce() && dt == CLIPMI_BF16) ? defer_ctx() : nullptr;
   // wgrad: C[M,N] += sum_tokens A[t][m] B[t][n]; the bf16 path also fuses the Linear bias
   // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
   auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                    float* bgrad) -> int {
     const int sp = wgrad_splits(M, N, R, dt);
     const bool fuse = dt == CLIPMI_BF16;
-    if (dctx && sp > 1) {  // deferred slab reduce: next slot, its previous reduce retired first
-      const int slot = dctx->next++ % NSLOT;
-      if (dctx->used[slot]) CLIPMI_HIP(hipStreamWaitEvent((hipStream_t)s, dctx->done[slot], 0));
-      const int64_t sb = split_bytes / NSLOT & ~(int64_t)255;
-      gemm_set_reduce_stream(dctx->side, dctx->after[slot]);
-      const int st = gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
-                          nullptr, 0, sp, (char*)wsplit + slot * sb, sb, bgrad);
-      gemm_set_reduce_stream(nullptr, nullptr);
-      CLIPMI_TRY(st);
-      CLIPMI_HIP(hipEventRecord(dctx->done[slot], dctx->side));
-      dctx->used[slot] = true;
-      return CLIPMI_OK;
-    }
     CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
                     nullptr, 0, sp, wsplit, split_bytes, fuse ? bgrad : nullptr));
     if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
@@ -375,10 +289,6 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
     CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
                                     g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
-  }
-  if (dctx) {  // every deferred reduce of this call lands before the caller's next work on s
-    CLIPMI_HIP(hipEventRecord(dctx->join, dctx->side));
-    CLIPMI_HIP(hipStreamWaitEvent((hipStream_t)s, dctx->join, 0));
   }
   return CLIPMI_OK;
 }

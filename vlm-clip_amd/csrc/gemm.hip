@@ -785,6 +785,7 @@ __global__ __launch_bounds__(256) void quant_mxfp8_kernel(const T* x, int64_t ld
   sc[r * nb + blk] = (uint8_t)(ex + 127);
 }
 
+#ifdef CLIPMI_GEMM_EXPERIMENTS  // persistent ping-pong (var 10) and half-tile pipeline (var 11): measured A/B forms
 // ------------------------------------------------------------------ persistent ping-pong
 // gemm_pp_kernel's schedule over a flattened stream of (tile, k-stage) pairs.  A workgroup
 // walks its tiles gridDim.x apart and the LDS ring runs straight across tile boundaries, so
@@ -1041,6 +1042,8 @@ __global__ __launch_bounds__(NT2, 1) void gemm_hp_kernel(GemmP p) {
   finish256<OutT, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, 0);
 }
 
+#endif  // CLIPMI_GEMM_EXPERIMENTS
+
 // ------------------------------------------------------------------ f32 SIMT path
 constexpr int FT = 64, FK = 16;
 
@@ -1196,6 +1199,7 @@ int num_cus() {
   }
   return n[dev];
 }
+#ifdef CLIPMI_GEMM_EXPERIMENTS
 template <bool AK, bool BKM, typename OutT, int EPI>
 void launch_pps(const GemmP& p, hipStream_t s) {
   (void)lds_optin((const void*)gemm_pps_kernel<AK, BKM, OutT, EPI>, PP_S * PP_STAGE);
@@ -1207,11 +1211,13 @@ void launch_hp(const GemmP& p, hipStream_t s) {
   (void)lds_optin((const void*)gemm_hp_kernel<BKM, OutT, EPI>, 131072);
   hipLaunchKernelGGL((gemm_hp_kernel<BKM, OutT, EPI>), dim3(p.ntiles), dim3(NT2), 131072, s, p);
 }
+#endif
 template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
 void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
-  // var 0 / 9: the ping-pong kernel; 10: its persistent form; 4: gemm256_kernel VAR 3
-  // (interleaved asm DMAs, the wgrad production schedule); 2 -> VAR 0 (all DMAs up front),
-  // 3 -> VAR 2 (builtin DMAs) for A/B.
+  // production: the 8-wave ping-pong kernel (var 0 / 9); var 4: gemm256_kernel VAR 3 (interleaved asm
+  // DMAs, round 2's weight-gradient schedule: the baseline of the 4-wave wgrad bitwise tests).  The
+  // measured-and-rejected schedules are compiled only into an EXTRA=-DCLIPMI_GEMM_EXPERIMENTS build.
+#ifdef CLIPMI_GEMM_EXPERIMENTS
   if (p.var == 10 && !BG && !p.ws && splits == 1) {
     launch_pps<AK, BKM, OutT, EPI>(p, s);
     return;
@@ -1223,23 +1229,22 @@ void launch256(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
     }
   }
   switch (p.var) {
-    case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
-    case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
-    case 4: launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
-    case 9: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
-    case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); break;  // no epilogue (timing)
-#ifdef CLIPMI_GEMM_EXPERIMENTS  // schedule A/B variants (measured, not production); build with EXTRA=-DCLIPMI_GEMM_EXPERIMENTS
-    case 13: launch_ppv<AK, BKM, OutT, EPI, BG, 16>(p, splits, s, bias_grad); break;  // DMAs between MFMAs
-    case 14: launch_ppv<AK, BKM, OutT, EPI, BG, 20>(p, splits, s, bias_grad); break;  // + no setprio
-    case 15: launch_ppv<AK, BKM, OutT, EPI, BG, 32>(p, splits, s, bias_grad); break;  // stores through LDS
-    case 16: launch_ppv<AK, BKM, OutT, EPI, BG, 64>(p, splits, s, bias_grad); break;  // direct stores only
-    case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); break;
-    case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); break;
-    case 7: launch_ppv<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); break;
-    case 8: launch_ppv<AK, BKM, OutT, EPI, BG, 4>(p, splits, s, bias_grad); break;
-#endif
-    default: launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); break;
+    case 2: launch256v<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad); return;   // all DMAs up front
+    case 3: launch256v<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); return;   // builtin DMAs
+    case 12: launch_ppv<AK, BKM, OutT, EPI, BG, 8>(p, splits, s, bias_grad); return;  // no epilogue (timing)
+    case 13: launch_ppv<AK, BKM, OutT, EPI, BG, 16>(p, splits, s, bias_grad); return;  // DMAs between MFMAs
+    case 14: launch_ppv<AK, BKM, OutT, EPI, BG, 20>(p, splits, s, bias_grad); return;  // + no setprio
+    case 15: launch_ppv<AK, BKM, OutT, EPI, BG, 32>(p, splits, s, bias_grad); return;  // stores through LDS
+    case 16: launch_ppv<AK, BKM, OutT, EPI, BG, 64>(p, splits, s, bias_grad); return;  // direct stores only
+    case 5: launch_ppv<AK, BKM, OutT, EPI, BG, 1>(p, splits, s, bias_grad); return;
+    case 6: launch_ppv<AK, BKM, OutT, EPI, BG, 2>(p, splits, s, bias_grad); return;
+    case 7: launch_ppv<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad); return;
+    case 8: launch_ppv<AK, BKM, OutT, EPI, BG, 4>(p, splits, s, bias_grad); return;
+    default: break;
   }
+#endif
+  if (p.var == 4) launch256v<AK, BKM, OutT, EPI, BG, 3>(p, splits, s, bias_grad);
+  else launch_ppv<AK, BKM, OutT, EPI, BG, 0>(p, splits, s, bias_grad);
 }
 
 constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU, E_G = CLIPMI_EPI_GELU;
@@ -1248,7 +1253,7 @@ constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
 
 const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
   if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
-    if (p.var == 28) {  // the persistent 4-wave kernel (gemm4.hip)
+    if (p.var == 28 || p.var == 31) {  // the persistent 4-wave kernel (gemm4.hip; 31: counted item-start wait)
       if (const char* l = dispatch_w4_wgrad(p, splits, s, flags, bg)) return l;
     }
     if (p.ws) {
@@ -1261,20 +1266,20 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     return "gemm256_wgrad";
   }
   if (bg) return nullptr;
+  // 28: the persistent 4-wave kernel for every shape; 31: the same with the counted item-start wait;
+  // 9: the 8-wave ping-pong kernel for every shape.  Experiments build only (CLIPMI_GEMM_EXPERIMENTS):
   // 20: 4-wave kernel, one tile per workgroup; 22-25: its stamped timing builds (22 production
   // schedule, 23 no main-loop DMAs, 24 no fragment reads, 25 neither)
-  // 28-30: the persistent 4-wave kernel (stagger 0 / 4 / 8 x s_sleep 127 for half of each XCD's CUs)
   // production (var 0): the persistent 4-wave kernel for long-K products (K >= 1536), where its main
   // loop is 3-7 % faster than the ping-pong kernel's; at K = 768 / 512 the ping-pong kernel's 8 waves
   // run the VALU-heavy epilogues twice as fast per SIMD (tools/w4_stamps.py, profiles/r03_*)
   // (and for fc2's input gradient with the stored-derivative product, K = 768: 1182 vs 1215 us,
   // profiles/r03_gemm_dact_shapes.log)
   const bool w4_default = p.var == 0 && (p.K >= 1536 || flags == E_MA);
-  if ((w4_default || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || (p.var >= 28 && p.var <= 30)) &&
+  if ((w4_default || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || p.var == 28 || p.var == 31) &&
       !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
     GemmP q = p;
-    if (p.var >= 28) q.stagger = (p.var - 28) * 4;
-    const int dm = (p.var >= 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
+    const int dm = p.var == 31 ? 101 : (p.var == 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
     if (const char* l = dispatch_w4(q, s, sel == 3, flags, dm)) return l;
   }
   if (sel == 3 && !f32o) {
@@ -1374,13 +1379,6 @@ extern "C" int clipmi_gemm_stamps(void* buf) {
   return CLIPMI_OK;
 }
 
-static thread_local hipStream_t g_reduce_stream = nullptr;
-static thread_local hipEvent_t g_after_gemm = nullptr;
-void gemm_set_reduce_stream(hipStream_t rs, hipEvent_t after_gemm) {
-  g_reduce_stream = rs;
-  g_after_gemm = after_gemm;
-}
-
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
@@ -1394,6 +1392,14 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_STORE_DACT) || (d->flags & (CLIPMI_EPI_QGELU | CLIPMI_EPI_GELU)),
                    "store_dact needs an activation flag");
     CLIPMI_REQUIRE((d->flags & ~1023) == 0, "unknown epilogue flag");
+    // aux has one role per launch, and the epilogues read one input stream besides it
+    constexpr int AUXR = CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU | CLIPMI_EPI_MUL_AUX;
+    constexpr int AUXW = CLIPMI_EPI_STORE_PRE | CLIPMI_EPI_STORE_DACT;
+    CLIPMI_REQUIRE((d->flags & AUXW) != AUXW, "store_pre and store_dact both write aux");
+    CLIPMI_REQUIRE(!((d->flags & AUXR) && (d->flags & AUXW)), "aux cannot be both read and written");
+    CLIPMI_REQUIRE(__builtin_popcount(d->flags & AUXR) <= 1, "at most one aux-reading flag");
+    CLIPMI_REQUIRE(!((d->flags & CLIPMI_EPI_MUL_AUX) && (d->flags & (CLIPMI_EPI_RESID | CLIPMI_EPI_BETA))),
+                   "mul_aux cannot be combined with residual / beta");
   }
   if (d->ab_dtype == CLIPMI_FP8) {  // MXFP8 operands (see include/clipmi.h)
     CLIPMI_REQUIRE(d->a_kmajor && d->b_kmajor, "fp8: both operands k-major");
@@ -1473,8 +1479,8 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.dbg = gemm_stamp_buffer();
   p.stagger = 0;
   p.first_round = num_cus();
-  if (d->force_small_tile >= 100) {  // A/B hook: 1xx ping-pong, 2xx persistent, with a stagger of xx
-    p.var = d->force_small_tile >= 200 ? 10 : 0;
+  if (d->force_small_tile >= 100) {  // A/B hook: 1xx the 8-wave ping-pong kernel with a first-round stagger of xx
+    p.var = 9;
     p.stagger = d->force_small_tile % 100;
   } else if (d->force_small_tile >= 2) p.var = d->force_small_tile;
   else if (evar >= 0 && d->force_small_tile == 0) p.var = evar;
@@ -1538,11 +1544,6 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   }
   CLIPMI_CHECK_LAUNCH();
   if (p.ws) {
-    if (g_reduce_stream && g_after_gemm) {  // the slab reduce on the engine's side stream
-      CLIPMI_HIP(hipEventRecord(g_after_gemm, s));
-      CLIPMI_HIP(hipStreamWaitEvent(g_reduce_stream, g_after_gemm, 0));
-      s = g_reduce_stream;
-    }
     const int64_t total = (int64_t)d->M * d->N;
     const int beta = (d->flags & CLIPMI_EPI_BETA) ? 1 : 0;
     if (d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0 && ((uintptr_t)p.ws & 15) == 0) {

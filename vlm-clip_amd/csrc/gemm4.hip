@@ -31,8 +31,6 @@
 //    per A fragment against a ones fragment (waves wn == 0 of n-tile 0), per-split partials summed
 //    in split order afterwards (deterministic).
 #include "gemm_common.h"
-#include <mutex>
-#include <vector>
 
 namespace cmg {
 namespace {
@@ -220,6 +218,27 @@ __device__ __forceinline__ void w4_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// s_waitcnt vmcnt(N) lgkmcnt(0) + barrier: retires every VMEM operation but the wave's N youngest.
+// At an item's start the youngest are the previous item's epilogue stores (issued after this
+// item's prologue DMAs): waiting for all but NSW of them lets the stores drain under the first
+// half-step instead of holding the barrier until the last write is acknowledged.
+template <int N>
+__device__ __forceinline__ void w4_sync_n() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// a lower bound on the global stores one wave's finish256x2 issues after the next item's prologue
+// DMAs (undercounting only waits longer): the LDS-staged bf16 epilogue stores 4 parts x 8 rows (x2
+// with a second output); every other path (fp32 slabs / beta, per-fragment stores) issues more
+template <typename OutT, int EPI>
+constexpr int w4_epi_stores() {
+  return std::is_same<OutT, bf16>::value ? ((EPI & (CLIPMI_EPI_STORE_PRE | CLIPMI_EPI_STORE_DACT)) ? 63 : 32) : 63;
+}
+
 template <bool AK, bool BKM>
 __device__ __forceinline__ void w4_stage_dma(char* img, const GemmP& p, const W4Lane& w, int wave, int m0, int n0,
                                              int k0, int kend, bool live) {
@@ -240,6 +259,7 @@ __device__ __forceinline__ void w4_first_frags(const char* smem, const W4Lane& w
   for (int j = 0; j < 8; ++j) b0[j] = w4_frag<BKM>(smem + w.b_rd[0], j, w.b_sw);
 }
 
+#ifdef CLIPMI_GEMM_EXPERIMENTS  // one tile per workgroup + stamped diagnostic builds (tools/w4_stamps.py)
 // ------------------------------------------------------------------ one tile per workgroup
 // The first form, kept for its diagnostic builds (ST: s_memtime stamps into LDS past the two
 // stages, copied to p.dbg: [0] kernel start, [1] main loop start, [2] main loop end, [3] kernel
@@ -339,15 +359,15 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
   }
 }
 
+#endif  // CLIPMI_GEMM_EXPERIMENTS
+
 // ------------------------------------------------------------------ persistent (production)
 // One workgroup per CU walks items i = r * grid + xcd_remap(blockIdx) (item = split * ntiles +
 // tile, so each XCD holds a contiguous run of one k-slab's tiles per round).  After an item's
 // main loop the next item's first two stages are DMA'd into the (now idle) stage buffers BEFORE
 // this item's epilogue runs, so the next prologue's latency hides behind the epilogue's stores;
-// the epilogue stages its rows in the 32 KiB past the two stages (8 KiB per wave).  p.stagger > 0:
-// half the workgroups of every XCD start p.stagger x s_sleep(127) later (A/B of desynchronised
-// epilogue bursts: measured neutral).
-template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+// the epilogue stages its rows in the 32 KiB past the two stages (8 KiB per wave).
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool CW>
 __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
@@ -360,9 +380,6 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   if (item >= nitems) return;
   const int lda = (int)p.lda, ldb = (int)p.ldb;
   const W4Lane w = w4_lane<AK, BKM>(wave, lane, p.lda, p.ldb);
-  if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   auto coords = [&](int it, int& m0, int& n0, int& kz, int& kbeg, int& kend) {
     kz = it / p.ntiles;
     int tm, tn;
@@ -385,16 +402,9 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   const bf16x8 ones = w4_ones();
   const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
-  // dynamic queue (p.dyn): after its first item (the static XCD-aware one) a workgroup takes the next
-  // unclaimed item from a counter, so a workgroup that started late -- its CU held by the other
-  // tower's stream -- takes fewer items instead of stretching the launch's tail.  Lane 0 of wave 0
-  // claims the next item at the start of the current one (a vector atomic: divergent lane), and the
-  // value reaches the other waves through LDS between two barriers after the main loop.
-  int claimed = 0;
   while (true) {
     int m0, n0, kz, kbeg, kend;
     coords(item, m0, n0, kz, kbeg, kend);
-    if (p.dyn && t == 0) claimed = atomicAdd(p.dyn, 1) + nwg;
     const int ns = (kend - kbeg + 63) / 64;
     const bool bias_wave = BG && n0 == 0 && wn == 0;
 #pragma unroll
@@ -407,33 +417,26 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
 #pragma unroll
       for (int i = 0; i < 8; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // this item's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed
-    w4_sync();
+    // this item's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed.
+    // CW: the previous item's epilogue stores (younger than these stages' DMAs) stay in flight
+    // through this sync and step 0's, whose stage 1 is also a prologue stage
+    constexpr int NSW = CW ? w4_epi_stores<OutT, EPI>() : 0;
+    w4_sync_n<NSW>();
     w4_first_frags<AK, BKM>(smem, w, a0, b0);
     for (int s = 0; s < ns; ++s) {
       char* img = smem + (s & 1) * W4_STAGE;
       char* nxt = smem + ((s + 1) & 1) * W4_STAGE;
       w4_half<AK, BKM, true, false, BG>(acc, accb, bias_wave, ones, a0, b0, a1, b1, img, 1, w, wave, nullptr, none, none, 0,
                                         0);
-      w4_sync();
+      if (CW && s == 0) w4_sync_n<NSW>();
+      else w4_sync();
       const bool more = s + 2 < ns;
       const SRsrc ra = w4_rsrc<AK>((const bf16*)p.A, p.lda, m0, p.M, kbeg + (s + 2) * 64, kend, more);
       const SRsrc rb = w4_rsrc<BKM>((const bf16*)p.B, p.ldb, n0, p.N, kbeg + (s + 2) * 64, kend, more);
       w4_half<AK, BKM, true, true, BG>(acc, accb, bias_wave, ones, a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb, lda, ldb);
     }
     w4_mfma_drain();
-    int next = item + nwg;
-    if (p.dyn) {  // broadcast the claimed item through the (idle) first stage, then free it again
-      // (vmcnt(0) first: the last step's empty-descriptor DMAs may still be writing zeros into a
-      // stage, and wave 0's first piece covers byte 0)
-      __builtin_amdgcn_s_waitcnt(0x0f70);
-      if (t == 0) *LDS_PTR(int, smem) = claimed;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
-      next = __builtin_amdgcn_readfirstlane(*LDS_PTR(const int, smem));
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();
-    }
+    const int next = item + nwg;
     // every wave's last useful stage read came before the last step's barrier (the final
     // half-step's reads fetch fragments nobody uses), so the next item may overwrite both stages
     if (next < nitems) prologue_dma(next);
@@ -452,64 +455,30 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
     if (next >= nitems) break;
     item = next;
   }
-  if (p.dyn && t == 0) {  // the last workgroup out resets both counters for the stream's next launch
-    __threadfence();
-    if (atomicAdd(p.dyn + 1, 1) == nwg - 1) {
-      atomicExch(p.dyn, 0);
-      atomicExch(p.dyn + 1, 0);
-    }
-  }
 }
 
-// persistent grid: one workgroup per CU, or fewer with CLIPMI_W4P_GRID (A/B of leaving CUs to the
-// other tower's stream: a persistent launch holds its CUs until its last item; read once)
-// dynamic-queue counters (CLIPMI_W4P_DYN=1, read once): one pair per stream, zeroed at allocation and
-// re-zeroed by each launch's last workgroup; launches on one stream are ordered, so they never overlap
-int* w4p_dyn_counters(hipStream_t s) {
-  static const bool on = [] {
-    const char* e = getenv("CLIPMI_W4P_DYN");
-    return e && atoi(e) != 0;
-  }();
-  if (!on) return nullptr;
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<int, hipStream_t>, int*>> tab;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> g(mu);
-  for (auto& e : tab)
-    if (e.first.first == dev && e.first.second == s) return e.second;
-  int* c = nullptr;
-  if (hipMalloc(&c, 2 * sizeof(int)) != hipSuccess) return nullptr;
-  if (hipMemset(c, 0, 2 * sizeof(int)) != hipSuccess) return nullptr;
-  tab.push_back({{dev, s}, c});
-  return c;
-}
-
-int w4p_max_grid() {
-  static const int g = [] {
-    const char* e = getenv("CLIPMI_W4P_GRID");
-    const int c = num_cus_w4();
-    return (e && atoi(e) > 0) ? std::min(atoi(e), c) : c;
-  }();
-  return g;
-}
-
-template <bool AK, bool BKM, typename OutT, int EPI, bool BG>
+// persistent grid: one workgroup per CU
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool CW = false>
 void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
-  (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>, L);
-  const int grid = std::min(p.ntiles * splits, w4p_max_grid());
-  GemmP q = p;
-  q.dyn = w4p_dyn_counters(s);
-  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG>), dim3(grid), dim3(W4_THR), L, s, q, bias_grad);
+  (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, CW>, L);
+  const int grid = std::min(p.ntiles * splits, num_cus_w4());
+  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, CW>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
 }
 
+// dm: 100 persistent, 101 persistent with the counted item-start wait; experiments build only:
+// 1 one tile per workgroup, < 0 the stamped diagnostic builds.  Returns false when not built.
 template <bool BKM, int EPI>
-void launch_w4(const GemmP& p, hipStream_t s, int dm) {
+bool launch_w4(const GemmP& p, hipStream_t s, int dm) {
   if (dm == 100) {
     launch_w4p<true, BKM, bf16, EPI, false>(p, 1, s, nullptr);
-    return;
+    return true;
   }
+  if (dm == 101) {
+    launch_w4p<true, BKM, bf16, EPI, false, true>(p, 1, s, nullptr);
+    return true;
+  }
+#ifdef CLIPMI_GEMM_EXPERIMENTS
   if (dm < 0) {  // diagnostic stamp builds
     constexpr int L = 2 * W4_STAGE + 4 * W4_NST * 8;
 #define W4_ST(n)                                                                                              \
@@ -520,10 +489,14 @@ void launch_w4(const GemmP& p, hipStream_t s, int dm) {
     else if (dm == -3) { W4_ST(2); }
     else { W4_ST(3); }
 #undef W4_ST
-    return;
+    return true;
   }
   (void)lds_optin((const void*)gemm_w4_kernel<BKM, bf16, EPI>, 2 * W4_STAGE);
   hipLaunchKernelGGL((gemm_w4_kernel<BKM, bf16, EPI>), dim3(p.ntiles), dim3(W4_THR), 2 * W4_STAGE, s, p);
+  return true;
+#else
+  return false;
+#endif
 }
 
 }  // namespace
@@ -537,19 +510,19 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
   constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
   if (bkm) {
     switch (flags) {
-      case E_B: launch_w4<true, E_B>(p, s, dm); return "gemm256_fwd_bias";
-      case E_B | E_R: launch_w4<true, E_B | E_R>(p, s, dm); return "gemm256_fwd_bias_resid";
-      case E_B | E_Q | E_P: launch_w4<true, E_B | E_Q | E_P>(p, s, dm); return "gemm256_fwd_bias_qgelu_pre";
-      case E_B | E_Q | E_DA: launch_w4<true, E_B | E_Q | E_DA>(p, s, dm); return "gemm256_fwd_bias_qgelu_dact";
-      case E_B | E_Q: launch_w4<true, E_B | E_Q>(p, s, dm); return "gemm256_fwd_bias_qgelu";
-      case 0: launch_w4<true, 0>(p, s, dm); return "gemm256_fwd";
+      case E_B: return launch_w4<true, E_B>(p, s, dm) ? "gemm256_fwd_bias" : nullptr;
+      case E_B | E_R: return launch_w4<true, E_B | E_R>(p, s, dm) ? "gemm256_fwd_bias_resid" : nullptr;
+      case E_B | E_Q | E_P: return launch_w4<true, E_B | E_Q | E_P>(p, s, dm) ? "gemm256_fwd_bias_qgelu_pre" : nullptr;
+      case E_B | E_Q | E_DA: return launch_w4<true, E_B | E_Q | E_DA>(p, s, dm) ? "gemm256_fwd_bias_qgelu_dact" : nullptr;
+      case E_B | E_Q: return launch_w4<true, E_B | E_Q>(p, s, dm) ? "gemm256_fwd_bias_qgelu" : nullptr;
+      case 0: return launch_w4<true, 0>(p, s, dm) ? "gemm256_fwd" : nullptr;
       default: return nullptr;
     }
   }
   switch (flags) {
-    case 0: launch_w4<false, 0>(p, s, dm); return "gemm256_dgrad";
-    case E_DQ: launch_w4<false, E_DQ>(p, s, dm); return "gemm256_dgrad_dqgelu";
-    case E_MA: launch_w4<false, E_MA>(p, s, dm); return "gemm256_dgrad_mulaux";
+    case 0: return launch_w4<false, 0>(p, s, dm) ? "gemm256_dgrad" : nullptr;
+    case E_DQ: return launch_w4<false, E_DQ>(p, s, dm) ? "gemm256_dgrad_dqgelu" : nullptr;
+    case E_MA: return launch_w4<false, E_MA>(p, s, dm) ? "gemm256_dgrad_mulaux" : nullptr;
     default: return nullptr;
   }
 }
@@ -558,6 +531,11 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
 // beta epilogue (one split), with the fused bias gradient when bg != nullptr
 const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg) {
   if (p.ws) {
+    if (p.var == 31) {
+      if (bg) launch_w4p<false, false, float, 0, true, true>(p, splits, s, bg);
+      else launch_w4p<false, false, float, 0, false, true>(p, splits, s, bg);
+      return "gemm256_wgrad_splitk";
+    }
     if (bg) launch_w4p<false, false, float, 0, true>(p, splits, s, bg);
     else launch_w4p<false, false, float, 0, false>(p, splits, s, bg);
     return "gemm256_wgrad_splitk";

@@ -590,6 +590,10 @@ __device__ __forceinline__ void epilogue_lds_pipe(const GemmP& p, f32x4 (&acc)[N
   constexpr bool HAUX = HDQ || HDG || HMA;
   constexpr bool HIN = HR || HAUX || HBETA;
   constexpr bool H2 = HPRE || HDA;  // a second output (aux), staged through LDS after the first
+  // one input stream (xin: res, else aux, else C) and one aux role per instance
+  static_assert(!(HMA && (HR || HBETA)), "MUL_AUX with RESID / BETA would read one input for both");
+  static_assert(!(HPRE && HDA), "STORE_PRE and STORE_DACT both write aux");
+  static_assert(!(HAUX && H2), "aux is either read or written");
   constexpr int NPART = 2 * NC;
   const int q = lane >> 4, mlane = lane & 15;
   const int coff = 16 * (q & 1) + 8 * (q >> 1);

@@ -31,10 +31,6 @@ inline hipError_t lds_optin(const void* fn, int bytes) {
 
 #define CLIPMI_TRY(call) do { int s_ = (call); if (s_ != CLIPMI_OK) return s_; } while (0)
 
-// Split-K reduce redirection (engine's deferred weight-gradient reduces): while set on this thread,
-// clipmi_gemm records `after_gemm` on its stream after a split-K GEMM, makes `rs` wait for it and
-// launches the slab reduce on `rs` instead of the GEMM's stream.
-void gemm_set_reduce_stream(hipStream_t rs, hipEvent_t after_gemm);
 
 // ---- live kernel profiler (clipmi_prof_*): while armed for a variant label, launches with
 // that label are bracketed by hipEvents on their own stream, so a caller can time one kernel
