@@ -169,6 +169,30 @@ def test_attention_bwd_single_pass(B, N, H, causal, monkeypatch):
         assert rel(dqkv[:, sl], qr.grad[:, sl]) < TOL[dtype] * 2, nm
 
 
+@pytest.mark.parametrize("qpw", ["2", "4"])
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 4, False), (3, 400, 2, True), (2, 197, 12, False)])
+def test_attention_flash_chunk_switch(qpw, B, N, H, causal, monkeypatch):
+    """CLIPMI_FA_QPW (the flash forward's query blocks per wave, i.e. 128- or 256-query chunks) keeps
+    the forward within the bf16 tolerance of the torch fp32 reference."""
+    monkeypatch.setenv("CLIPMI_ATTN_FA", "1")
+    monkeypatch.setenv("CLIPMI_FA_QPW", qpw)
+    dtype = torch.bfloat16
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 41, dtype)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(42)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    o = torch.empty(B * N, D, dtype=dtype, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    T.call("clipmi_attention_fwd", kern.stream(), DT[dtype], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(),
+           mask.data_ptr() if mask is not None else None, int(causal), B, H, N, D)
+    oref, lref = attn_ref(qkv.float(), B, N, H, mask, causal)
+    assert rel(o, oref) < TOL[dtype]
+    assert (lse - lref).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_text_embedding_fwd_bwd(dtype):
     B, S, D, V = 6, 77, 512, 1000
