@@ -150,21 +150,24 @@ def _mx8_exact(R, K, seed):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 520, 256), (1024, 768, 1024), (77, 64, 640),
-                                   (256, 256, 384), (2304, 1280, 4096)])
-def test_gemm_fp8_block_scaled_exact(M, N, K):
-    """v_mfma_scale_f32_16x16x128_f8f6f4 GEMM: integer operands and power-of-two block scales make
-    every product and sum exact in fp32, so the result must equal the dequantised product exactly
-    (checks the fp8 fragment map and which lanes' scale bytes apply to which k-blocks)."""
+                                   (256, 256, 384), (2304, 1280, 4096), (1000, 1100, 768), (4096, 512, 2048)])
+@pytest.mark.parametrize("variant", [0, 40, 41])
+def test_gemm_fp8_block_scaled_exact(M, N, K, variant):
+    """v_mfma_scale_f32_32x32x64_f8f6f4 GEMMs (0: production dispatch; 40: the 8-wave kernel everywhere;
+    41: the persistent 4-wave kernel wherever K % 256 == 0 and M, N >= 256): integer operands and power-of-two
+    block scales make every product and sum exact in fp32, so the result must equal the dequantised
+    product exactly (checks the fp8 fragment map and which lanes' scale bytes apply to which k-blocks)."""
     A, B = _mx8_exact(M, K, 1), _mx8_exact(N, K, 2)
     C = torch.empty(M, N, device="cuda", dtype=torch.float32)
-    kern.gemm_fp8(M, N, K, A, B, C, N)
+    kern.gemm_fp8(M, N, K, A, B, C, N, variant=variant)
     ref = A.dequant() @ B.dequant().t()
     torch.cuda.synchronize()
     assert torch.equal(C, ref), (C - ref).abs().max().item()
 
 
 @pytest.mark.parametrize("flags", [0, _lib.EPI_BIAS, _lib.EPI_BIAS | _lib.EPI_RESID, _lib.EPI_BIAS | _lib.EPI_QGELU])
-def test_gemm_fp8_epilogues(flags):
+@pytest.mark.parametrize("variant", [0, 40, 41])
+def test_gemm_fp8_epilogues(flags, variant):
     M, N, K = 600, 384, 512
     x = _mk((M, K), torch.bfloat16, 21)
     w = _mk((N, K), torch.bfloat16, 22) * 0.05
@@ -172,7 +175,7 @@ def test_gemm_fp8_epilogues(flags):
     bias = _mk((N,), torch.bfloat16, 23)
     res = _mk((M, N), torch.bfloat16, 24)
     C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, residual=res, ldr=N, flags=flags)
+    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, residual=res, ldr=N, flags=flags, variant=variant)
     acc = A.dequant() @ B.dequant().t()
     ref, _ = _ref_epi(acc, flags, bias, None, res)
     torch.cuda.synchronize()
@@ -212,7 +215,8 @@ def _mx_close(m, ref, frac=0.99):
     assert (err <= 0).all(), err.max().item()
 
 
-def test_gemm_fp8_mxfp8_output():
+@pytest.mark.parametrize("variant", [0, 40, 41])
+def test_gemm_fp8_mxfp8_output(variant):
     """fc1's fused epilogue in the fp8 towers: bias + quick_gelu, written as MXFP8 [M, N] + scales."""
     M, N, K = 600, 512, 512
     x = _mk((M, K), torch.bfloat16, 31)
@@ -222,7 +226,7 @@ def test_gemm_fp8_mxfp8_output():
     C = kern.MX8(torch.empty(M, N, dtype=torch.uint8, device="cuda"),
                  torch.empty(M, N // 32, dtype=torch.uint8, device="cuda"))
     flags = _lib.EPI_BIAS | _lib.EPI_QGELU
-    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, flags=flags)
+    kern.gemm_fp8(M, N, K, A, B, C, N, bias=bias, flags=flags, variant=variant)
     acc = A.dequant() @ B.dequant().t()
     ref, _ = _ref_epi(acc, flags, bias, None, None)
     torch.cuda.synchronize()
@@ -252,7 +256,7 @@ def test_layernorm_mxfp8(R, D):
     assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
 
 
-@pytest.mark.parametrize("var", [28, 31])
+@pytest.mark.parametrize("var", [28, 32])
 @pytest.mark.parametrize("bkm,flags", [
     (True, _lib.EPI_BIAS), (True, _lib.EPI_BIAS | _lib.EPI_RESID),
     (True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE), (True, _lib.EPI_BIAS | _lib.EPI_QGELU), (True, 0),
@@ -290,7 +294,7 @@ def test_gemm_4wave_matches_pingpong(var, bkm, flags, M, N, K):
                                               (20000, 2304, 768, 4), (300, 768, 768, 3), (4100, 520, 264, 2),
                                               (9000, 768, 768, 1)])
 @pytest.mark.parametrize("bias", [False, True])
-@pytest.mark.parametrize("var", [28, 31])
+@pytest.mark.parametrize("var", [28, 32])
 def test_wgrad_4wave_matches_8wave(T, Nout, Kin, split, bias, var):
     """Weight gradient on the persistent 4-wave kernel (gemm4.hip, variant 28) vs the 8-wave wgrad
     kernel (variant 4): the same k order of MFMA accumulation per output element, so bitwise-equal
@@ -312,3 +316,23 @@ def test_wgrad_4wave_matches_8wave(T, Nout, Kin, split, bias, var):
         assert torch.equal(outs[0][1], outs[1][1])
     ref = C0 + dY.float().t() @ X.float()
     assert (outs[1][0] - ref).abs().max().item() / ref.abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("raster", ["0", "4", "8"])
+@pytest.mark.parametrize("var", [9, 28])
+def test_gemm_raster_groups_bitwise(raster, var, monkeypatch):
+    """CLIPMI_RASTER (tile-rows per rasterisation group) only reorders the tiles: every output
+    element keeps its k order, so the result is bitwise equal to row-major order (both the 8-wave
+    and the persistent 4-wave kernel; 3000 rows = 12 ragged tile-rows)."""
+    M, N, K = 3000, 776, 768
+    A = _mk((M, K), torch.bfloat16, 51)
+    B = _mk((N, K), torch.bfloat16, 52)
+    bias = _mk((N,), torch.bfloat16, 53)
+    outs = []
+    for r in ("0", raster):
+        monkeypatch.setenv("CLIPMI_RASTER", r)
+        C = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        kern.gemm(M, N, K, A, K, True, B, K, True, C, N, bias=bias, flags=_lib.EPI_BIAS, small_tile=var)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])

@@ -23,8 +23,8 @@ def main(path):
     for i, l in enumerate(ins):
         if not l.startswith("v_mfma"):
             continue
-        ops = [o.strip() for o in l.split(None, 1)[1].split(",")]
-        srcs = set().union(*(regs(o) for o in ops[1:4]))
+        ops = [o.strip().split()[0] for o in l.split(None, 1)[1].split(",")]
+        srcs = set().union(*(regs(o) for o in ops[1:]))  # A, B, C and (v_mfma_scale) the two scale operands
         for back in (1, 2):
             p = ins[i - back] if i >= back else ""
             if p.startswith("s_nop"):

@@ -14,6 +14,8 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 R, D, F = B * 577, 1024, 4096
 REPS = int(os.environ.get("FP8_REPS", "10"))
 ONLY = os.environ.get("FP8_SHAPES", "").split(",") if os.environ.get("FP8_SHAPES") else None
+# FP8_VARIANTS=0,40: the production dispatch (persistent 4-wave kernel where it applies) and the 8-wave kernel
+VARIANTS = [int(v) for v in os.environ.get("FP8_VARIANTS", "0").split(",")]
 
 
 def timeit(f, n=REPS):
@@ -35,6 +37,11 @@ def mx(r, c):
 
 
 torch.manual_seed(0)
+_w = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+for _ in range(100):  # clock warm-up
+    _w @ _w
+torch.cuda.synchronize()
+del _w
 if os.environ.get("FP8_KSWEEP"):  # time(K) = per-tile fixed cost + K/64 stages: split them (N = 3072, bias)
     for Kd in (128, 256, 512, 1024, 2048, 4096):
         x = (torch.randn(R, Kd, device="cuda") * 0.5).to(torch.bfloat16)
@@ -62,15 +69,17 @@ for name, N, Kd, flags, q8o in (("qkv", 3 * D, D, _lib.EPI_BIAS, False),
     res = torch.randn(R, N, device="cuda").to(torch.bfloat16) if flags & _lib.EPI_RESID else None
     A, Bq = K.quant_mxfp8(x), K.quant_mxfp8(w)
     C = mx(R, N) if q8o else torch.empty(R, N, device="cuda", dtype=torch.bfloat16)
-    f8 = lambda: K.gemm_fp8(R, N, Kd, A, Bq, C, N, bias=bias, residual=res, ldr=N, flags=flags)
-    ms8 = timeit(f8)
     fl = 2.0 * R * N * Kd
-    line = f"{name:7s} M={R} N={N} K={Kd}: fp8 {ms8 * 1e3:8.1f} us {fl / ms8 / 1e9:7.1f} TF/s"
+    line = f"{name:7s} M={R} N={N} K={Kd}:"
+    for v in VARIANTS:
+        f8 = lambda: K.gemm_fp8(R, N, Kd, A, Bq, C, N, bias=bias, residual=res, ldr=N, flags=flags, variant=v)
+        ms8 = timeit(f8)
+        line += f" fp8 v{v} {ms8 * 1e3:8.1f} us {fl / ms8 / 1e9:7.1f} TF/s |"
     if not q8o:
         Cb = torch.empty(R, N, device="cuda", dtype=torch.bfloat16)
         fb = lambda: K.gemm(R, N, Kd, x, Kd, True, w, Kd, True, Cb, N, bias=bias, residual=res, ldr=N, flags=flags)
         msb = timeit(fb)
-        line += f" | bf16 {msb * 1e3:8.1f} us {fl / msb / 1e9:7.1f} TF/s"
+        line += f" bf16 {msb * 1e3:8.1f} us {fl / msb / 1e9:7.1f} TF/s"
     print(line, flush=True)
     del x, w, A, Bq, C, res
     torch.cuda.empty_cache()

@@ -137,7 +137,7 @@ def layernorm_mxfp8(x, w, b, eps=1e-5):
     return out, mean, rstd
 
 
-def gemm_fp8(M, N, K, A, B, C, ldc, *, bias=None, residual=None, ldr=0, alpha=1.0, flags=0):
+def gemm_fp8(M, N, K, A, B, C, ldc, *, bias=None, residual=None, ldr=0, alpha=1.0, flags=0, variant=0):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)) with A [M, K], B [N, K] MXFP8 (MX8).  C is a
     tensor (bf16 / fp32) or an MX8 [M, N] (MXFP8 output: flags bias / activation only)."""
     q8o = isinstance(C, MX8)
@@ -155,5 +155,6 @@ def gemm_fp8(M, N, K, A, B, C, ldc, *, bias=None, residual=None, ldr=0, alpha=1.
     d.ab_dtype, d.c_dtype = FP8, (FP8 if q8o else dt(C))
     d.bias_dtype = dt(bias) if bias is not None else F32
     d.split_k = 1
+    d.force_small_tile = int(variant)  # 40: the 8-wave fp8 kernel instead of the persistent 4-wave one
     _lib.check(_lib.lib().clipmi_gemm(stream(), ctypes.byref(d)), "clipmi_gemm")
     return C

@@ -1431,10 +1431,8 @@ void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s) {
 
 int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
   const bool masked = causal || p.kmask;
-  static const int env_qpw = [] {  // A/B hook: CLIPMI_FA_QPW=2|4 forces the chunk size
-    const char* e = getenv("CLIPMI_FA_QPW");
-    return e ? atoi(e) : 0;
-  }();
+  const char* e = getenv("CLIPMI_FA_QPW");  // A/B hook (read per call): 2|4 forces the chunk size
+  const int env_qpw = e ? atoi(e) : 0;
   const int qpw = env_qpw == 2 || env_qpw == 4 ? env_qpw : (p.N > 256 ? 4 : 2);
   if (qpw == 4) {  // 256-query chunks: K/V streamed once per 256 queries
     if (masked) launch_fwd_fa<4, true>(p, causal, s); else launch_fwd_fa<4, false>(p, causal, s);

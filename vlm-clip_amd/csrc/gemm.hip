@@ -444,8 +444,6 @@ __global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmP p, float* bias_gr
 // ([rows][K/32] bytes: the OCP MX layout), on v_mfma_scale_f32_32x32x64_f8f6f4 (twice the bf16
 // MFMA rate; the hardware applies both operands' block scales inside the MFMA).  Epilogues: the
 // bf16 kernels' finish256 after a register-layout conversion, or MXFP8 output (epilogue_q8).
-typedef __attribute__((ext_vector_type(8))) int i32x8;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 // Operand map of v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3), measured with exact data
 // (tools/probes/mfma_f8f6f4_32x32_layout.hip, profiles/r02_f8f6f4_32x32_layout.txt): lane l holds
@@ -475,65 +473,6 @@ __device__ __forceinline__ void stage_pp8(char* img, const uint8_t* X, int64_t l
     const int r = 16 * j + (lane >> 2);
     const int c = (lane & 3) ^ ((r >> 2) & 3);
     dma16(rs, img + j * 1024, (int)((int64_t)r * ld + c * 16));
-  }
-}
-
-// MXFP8 output (fc1 -> fc2 in the fp8 towers): alpha, bias, activation, then per 32-column
-// block of a row -- the 8-column pieces of lanes mlane + 16q, q = 0..3 (epilogue256_lds's
-// permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3 bytes (8 B per lane).
-template <int EPI>
-__device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
-  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
-  const int q = lane >> 4, mlane = lane & 15;
-  const int coff = 16 * (q & 1) + 8 * (q >> 1);
-  uint8_t* out = (uint8_t*)p.C;
-  const int nsb = p.N >> 5;
-  float bv[2][8];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    const int n = min(nb + 32 * jp + coff, p.N - 8);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
-    if (HB) {
-      if (p.bias_f32) {
-        load4((const float*)p.bias + n, bv[jp]);
-        load4((const float*)p.bias + n + 4, bv[jp] + 4);
-      } else {
-        load8((const bf16*)p.bias + n, bv[jp]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mb + i * 16 + mlane;
-#pragma unroll
-    for (int jp = 0; jp < 2; ++jp) {
-      const int n = nb + 32 * jp + coff;
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
-                                                         __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
-        v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
-        v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
-      }
-      float am = 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if (HQ) v[r] = quick_gelu(v[r]);
-        if (HG) v[r] = gelu_erf(v[r]);
-        am = fmaxf(am, fabsf(v[r]));
-      }
-      am = fmaxf(am, __shfl_xor(am, 16, 64));
-      am = fmaxf(am, __shfl_xor(am, 32, 64));
-      const int ex = mx_exponent(am);
-      const float inv = ldexpf(1.0f, -ex);
-      const uint32_t w0 = mx_pack4(v[0], v[1], v[2], v[3], inv), w1 = mx_pack4(v[4], v[5], v[6], v[7], inv);
-      if (m < p.M && n < p.N) {
-        *(u32x2*)(out + (int64_t)m * p.ldc + n) = u32x2{w0, w1};
-        if (q == 0) p.c_scale[(int64_t)m * nsb + ((nb + 32 * jp) >> 5)] = (uint8_t)(ex + 127);
-      }
-    }
   }
 }
 
@@ -724,6 +663,7 @@ void launch_fp8(const GemmP& p, hipStream_t s) {
 }
 
 const char* dispatch_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, int flags) {
+  if (const char* l = dispatch_w4_fp8(p, s, f32o, q8o, flags)) return l;  // the persistent 4-wave form
   if (q8o) {
     switch (flags) {
       case E8_B | E8_Q: launch_fp8<uint8_t, E8_B | E8_Q>(p, s); return "gemm_fp8_fwd_bias_qgelu_q8";
@@ -1253,7 +1193,7 @@ constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
 
 const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
   if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
-    if (p.var == 28 || p.var == 31) {  // the persistent 4-wave kernel (gemm4.hip; 31: counted item-start wait)
+    if (p.var == 28 || p.var == 32) {  // the persistent 4-wave kernel (gemm4.hip; 32: with the L2 prefetch)
       if (const char* l = dispatch_w4_wgrad(p, splits, s, flags, bg)) return l;
     }
     if (p.ws) {
@@ -1266,8 +1206,8 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     return "gemm256_wgrad";
   }
   if (bg) return nullptr;
-  // 28: the persistent 4-wave kernel for every shape; 31: the same with the counted item-start wait;
-  // 9: the 8-wave ping-pong kernel for every shape.  Experiments build only (CLIPMI_GEMM_EXPERIMENTS):
+  // 28: the persistent 4-wave kernel for every shape; 32: the same with the L2 prefetch of the
+  // activation operand; 9: the 8-wave ping-pong kernel for every shape.  Experiments build only (CLIPMI_GEMM_EXPERIMENTS):
   // 20: 4-wave kernel, one tile per workgroup; 22-25: its stamped timing builds (22 production
   // schedule, 23 no main-loop DMAs, 24 no fragment reads, 25 neither)
   // production (var 0): the persistent 4-wave kernel for long-K products (K >= 1536), where its main
@@ -1275,11 +1215,16 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
   // run the VALU-heavy epilogues twice as fast per SIMD (tools/w4_stamps.py, profiles/r03_*)
   // (and for fc2's input gradient with the stored-derivative product, K = 768: 1182 vs 1215 us,
   // profiles/r03_gemm_dact_shapes.log)
+  // and, with the L2 prefetch of the activation operand (gemm4.hip w4_prefetch), for the short-K input
+  // gradients (fc2's with the stored-derivative product, and out-proj's K = 768): 1.2-1.5 % and
+  // 3-4 % over the persistent kernel without it (profiles/r04_gemm_variants.log); the forward shapes
+  // and the long-K products measured equal or slower with it
+  const bool w4_pf = p.var == 0 && sel == 2 && (flags == E_MA || (flags == 0 && p.K <= 768));
   const bool w4_default = p.var == 0 && (p.K >= 1536 || flags == E_MA);
-  if ((w4_default || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || p.var == 28 || p.var == 31) &&
+  if ((w4_default || w4_pf || p.var == 20 || (p.var >= 22 && p.var <= 25 && p.dbg) || p.var == 28 || p.var == 32) &&
       !f32o && !p.ws && splits == 1 && (sel == 3 || sel == 2)) {
     GemmP q = p;
-    const int dm = p.var == 31 ? 101 : (p.var == 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
+    const int dm = (p.var == 32 || w4_pf) ? 102 : (p.var == 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
     if (const char* l = dispatch_w4(q, s, sel == 3, flags, dm)) return l;
   }
   if (sel == 3 && !f32o) {
@@ -1356,10 +1301,8 @@ const char* dispatch_bf16(const GemmP& p, int splits, hipStream_t s, bool f32o, 
 // Defaults from profiles/r02_raster_ab.log: bf16 row-major (groups of 4/8/16: within +-3 %, no
 // consistent winner), fp8 groups of 8 (fc1 +10 %, the rest neutral).
 int raster_rows(bool fp8 = false) {
-  static const int r = [] {
-    const char* e = getenv("CLIPMI_RASTER");
-    return e ? atoi(e) : -1;
-  }();
+  const char* e = getenv("CLIPMI_RASTER");  // read per call (tests switch it at run time)
+  const int r = e ? atoi(e) : -1;
   return r >= 0 ? r : (fp8 ? 8 : 0);
 }
 
@@ -1424,6 +1367,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     p.b_scale = (const uint8_t*)d->b_scale;
     p.c_scale = d->c_scale;
     p.raster = raster_rows(true);
+    p.var = d->force_small_tile;  // 40: the 8-wave fp8 kernel (A/B of the persistent 4-wave one)
     p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
             ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
     p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&

@@ -219,9 +219,8 @@ __device__ __forceinline__ void w4_sync() {
 }
 
 // s_waitcnt vmcnt(N) lgkmcnt(0) + barrier: retires every VMEM operation but the wave's N youngest.
-// At an item's start the youngest are the previous item's epilogue stores (issued after this
-// item's prologue DMAs): waiting for all but NSW of them lets the stores drain under the first
-// half-step instead of holding the barrier until the last write is acknowledged.
+// (An item-start form that left the previous epilogue's stores in flight, vmcnt(32 / 63), measured
+// neutral: profiles/r04_gemm_variants.log.)
 template <int N>
 __device__ __forceinline__ void w4_sync_n() {
   static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
@@ -231,12 +230,22 @@ __device__ __forceinline__ void w4_sync_n() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// a lower bound on the global stores one wave's finish256x2 issues after the next item's prologue
-// DMAs (undercounting only waits longer): the LDS-staged bf16 epilogue stores 4 parts x 8 rows (x2
-// with a second output); every other path (fp32 slabs / beta, per-fragment stores) issues more
-template <typename OutT, int EPI>
-constexpr int w4_epi_stores() {
-  return std::is_same<OutT, bf16>::value ? ((EPI & (CLIPMI_EPI_STORE_PRE | CLIPMI_EPI_STORE_DACT)) ? 63 : 32) : 63;
+// L2 prefetch of one streamed operand's 256x64 k-stage: one dword per 128-B line of the stage's tile
+// (this wave's quarter: 64 lines), LDS-DMA'd into this wave's epilogue staging area, which the main
+// loop leaves idle (LDS-DMA needs no destination registers, so no late write can land in a VGPR the
+// compiler has reused).  Measured motivation (tools/w4p_stamps.py, profiles/r04_w4p_stamps.log): with
+// the activation operand's rows aliased into the CU's own cache the k-step drops from ~3.45k to
+// ~2.88k cycles -- the nine CUs that share an activation panel all miss in L2 on the same k-slice at
+// the same moment and wait for one HBM fetch; the weights (MALL / L2) are not the bottleneck.
+// Two dwords per line (bytes 0 and 64): the L2 allocates 64-B halves on a partial-line miss.
+template <bool KMAJ>
+__device__ __forceinline__ void w4_prefetch(const SRsrc& r, char* scratch, int wave, int lane, int ld) {
+  const int l = wave * 64 + lane;
+  const int voff = KMAJ ? l * ld * 2 : (l >> 2) * ld * 2 + (l & 3) * 128;
+  const uint32_t m = (uint32_t)(uintptr_t)LDS_PTR(char, scratch);
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+               "buffer_load_dword %1, %2, 0 offen offset:64 lds" ::"s"(m), "v"(voff), "s"(r.v)
+               : "memory");
 }
 
 template <bool AK, bool BKM>
@@ -367,10 +376,39 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
 // main loop the next item's first two stages are DMA'd into the (now idle) stage buffers BEFORE
 // this item's epilogue runs, so the next prologue's latency hides behind the epilogue's stores;
 // the epilogue stages its rows in the 32 KiB past the two stages (8 KiB per wave).
-template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool CW>
+// CLIPMI_W4P_STAMPS (diagnostic build only, tools/w4p_stamps.py): per workgroup < 256, wave and
+// item < 20, s_memtime at the item's top, after its start sync, after its main loop, after the next
+// item's prologue DMAs and after its epilogue, into p.dbg[(blk * 4 + wave) * 128 + item * 6 + phase];
+// [126] / [127] s_memrealtime and [125] / [124] s_memtime at kernel start / end (lane 0, plain
+// vector stores).
+#ifdef CLIPMI_W4P_STAMPS
+#define W4P_ST(ph)                                                                                     \
+  do {                                                                                                 \
+    if (p.dbg && blockIdx.x < 256 && it_no < 20 && lane == 0)                                          \
+      p.dbg[(blockIdx.x * 4 + wave) * 128 + it_no * 6 + (ph)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
+#else
+#define W4P_ST(ph) do { } while (0)
+#endif
+
+// PF: L2 prefetch of the streamed operands (A always; B too for the weight gradient, whose B is the
+// activation X) PF_D stages ahead, issued after each second half-step's DMAs (w4_prefetch); the next
+// sync then waits vmcnt(NPF) so the prefetch stays in flight, and a prefetch is required complete
+// one step later (it is older than that step's DMAs).  None in the last two steps of an item: the
+// epilogue reuses the prefetches' LDS scratch; the next item's stages 0 and 1 are prefetched from
+// this item's steps ns - 4 and ns - 3 instead.
+constexpr int PF_D = 4;
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool PF = false>
 __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bias_grad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
+#ifdef CLIPMI_W4P_STAMPS
+  int it_no = 0;
+  if (p.dbg && blockIdx.x < 256 && lane == 0) {
+    p.dbg[(blockIdx.x * 4 + (t >> 6)) * 128 + 126] = __builtin_amdgcn_s_memrealtime();
+    p.dbg[(blockIdx.x * 4 + (t >> 6)) * 128 + 125] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nwg = gridDim.x;
@@ -402,10 +440,18 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   const bf16x8 ones = w4_ones();
   const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
+  constexpr bool PFB = PF && !BKM && !AK;  // weight gradient: B is streamed too
+  constexpr int NPF = PF ? (PFB ? 4 : 2) : 0;  // prefetch instructions per step
+  char* const pf_area = smem + 2 * W4_STAGE + wave * 8192;
   while (true) {
     int m0, n0, kz, kbeg, kend;
     coords(item, m0, n0, kz, kbeg, kend);
     const int ns = (kend - kbeg + 63) / 64;
+    int nm0 = 0, nn0 = 0, nkbeg = 0, nkend = 0;
+    if (PF && item + nwg < nitems) {
+      int nkz;
+      coords(item + nwg, nm0, nn0, nkz, nkbeg, nkend);
+    }
     const bool bias_wave = BG && n0 == 0 && wn == 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -417,29 +463,44 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
 #pragma unroll
       for (int i = 0; i < 8; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // this item's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed.
-    // CW: the previous item's epilogue stores (younger than these stages' DMAs) stay in flight
-    // through this sync and step 0's, whose stage 1 is also a prologue stage
-    constexpr int NSW = CW ? w4_epi_stores<OutT, EPI>() : 0;
-    w4_sync_n<NSW>();
+    // this item's stages 0 and 1 landed (every wave), the previous epilogue's LDS rows consumed
+    W4P_ST(0);
+    w4_sync();
+    W4P_ST(1);
     w4_first_frags<AK, BKM>(smem, w, a0, b0);
     for (int s = 0; s < ns; ++s) {
       char* img = smem + (s & 1) * W4_STAGE;
       char* nxt = smem + ((s + 1) & 1) * W4_STAGE;
       w4_half<AK, BKM, true, false, BG>(acc, accb, bias_wave, ones, a0, b0, a1, b1, img, 1, w, wave, nullptr, none, none, 0,
                                         0);
-      if (CW && s == 0) w4_sync_n<NSW>();
+      if (PF && s >= 1 && s - 1 <= ns - 3) w4_sync_n<NPF>();  // the previous step's prefetch stays in flight
       else w4_sync();
       const bool more = s + 2 < ns;
       const SRsrc ra = w4_rsrc<AK>((const bf16*)p.A, p.lda, m0, p.M, kbeg + (s + 2) * 64, kend, more);
       const SRsrc rb = w4_rsrc<BKM>((const bf16*)p.B, p.ldb, n0, p.N, kbeg + (s + 2) * 64, kend, more);
       w4_half<AK, BKM, true, true, BG>(acc, accb, bias_wave, ones, a1, b1, a0, b0, nxt, 0, w, wave, img, ra, rb, lda, ldb);
+      if (PF && s <= ns - 3) {
+        // target: stage s + PF_D of this item, else stage s + PF_D - ns of the next one (its stages
+        // 0 and 1 from steps ns - 4 and ns - 3); an empty descriptor past either item's end
+        const int tj = s + PF_D;
+        const bool mine = tj < ns;
+        const int pj = mine ? tj : tj - ns;
+        const int pm0 = mine ? m0 : nm0, pn0 = mine ? n0 : nn0;
+        const int pkb = mine ? kbeg : nkbeg, pke = mine ? kend : nkend;
+        const bool live = mine || (pj <= 1 && pke > pkb + pj * 64);
+        w4_prefetch<AK>(w4_rsrc<AK>((const bf16*)p.A, p.lda, pm0, p.M, pkb + pj * 64, pke, live), pf_area, wave, lane, lda);
+        if (PFB)
+          w4_prefetch<BKM>(w4_rsrc<BKM>((const bf16*)p.B, p.ldb, pn0, p.N, pkb + pj * 64, pke, live), pf_area, wave, lane,
+                           ldb);
+      }
     }
     w4_mfma_drain();
+    W4P_ST(2);
     const int next = item + nwg;
     // every wave's last useful stage read came before the last step's barrier (the final
     // half-step's reads fetch fragments nobody uses), so the next item may overwrite both stages
     if (next < nitems) prologue_dma(next);
+    W4P_ST(3);
     if (BG && bias_wave && lane < 16) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -452,21 +513,31 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
     }
     char* st = smem + 2 * W4_STAGE + wave * 8192;
     finish256x2<OutT, EPI, true>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, kz, st);
+    W4P_ST(4);
+#ifdef CLIPMI_W4P_STAMPS
+    ++it_no;
+#endif
     if (next >= nitems) break;
     item = next;
   }
+#ifdef CLIPMI_W4P_STAMPS
+  if (p.dbg && blockIdx.x < 256 && lane == 0) {
+    p.dbg[(blockIdx.x * 4 + wave) * 128 + 124] = __builtin_amdgcn_s_memtime();
+    p.dbg[(blockIdx.x * 4 + wave) * 128 + 127] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // persistent grid: one workgroup per CU
-template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool CW = false>
+template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool PF = false>
 void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
-  (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, CW>, L);
+  (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, PF>, L);
   const int grid = std::min(p.ntiles * splits, num_cus_w4());
-  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, CW>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
+  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, PF>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
 }
 
-// dm: 100 persistent, 101 persistent with the counted item-start wait; experiments build only:
+// dm: 100 persistent, 102 persistent with the L2 prefetch; experiments build only:
 // 1 one tile per workgroup, < 0 the stamped diagnostic builds.  Returns false when not built.
 template <bool BKM, int EPI>
 bool launch_w4(const GemmP& p, hipStream_t s, int dm) {
@@ -474,7 +545,7 @@ bool launch_w4(const GemmP& p, hipStream_t s, int dm) {
     launch_w4p<true, BKM, bf16, EPI, false>(p, 1, s, nullptr);
     return true;
   }
-  if (dm == 101) {
+  if (dm == 102) {  // L2 prefetch of the activation operand
     launch_w4p<true, BKM, bf16, EPI, false, true>(p, 1, s, nullptr);
     return true;
   }
@@ -499,6 +570,276 @@ bool launch_w4(const GemmP& p, hipStream_t s, int dm) {
 #endif
 }
 
+
+// ------------------------------------------------------------------ MXFP8 (config 5)
+// The persistent 4-wave schedule with MXFP8 operands (OCP e4m3, one E8M0 scale per 32 k of a row;
+// BASELINE config 5's frozen ViT-L/14@336 towers) on v_mfma_scale_f32_32x32x64_f8f6f4, which runs
+// at twice the bf16 rate.  gemm.hip's gemm_fp8_kernel kept the 8-wave ping-pong stage time while
+// each stage carried twice the FLOPs (PMC: 24-27 % of the fp8 pipe busy); here a stage is 128 k
+// = 256 rows x 128 B per operand, byte for byte the bf16 4-wave kernel's 64-k stage, so the same
+// LDS images, DMA pieces and swizzle serve it (the fp8 buffers are addressed as bf16 pairs) and a
+// stage carries 2 x 16 MFMAs of 64 cycles per wave = the bf16 kernel's 2048 matrix-pipe cycles
+// per 64 KiB.  Per wave 128 x 128 = 4 x 4 blocks of 32 x 32 (16 f32x16 accumulators pinned in the
+// AGPRs by inline-asm MFMAs).  Operand map (profiles/r02_f8f6f4_32x32_layout.txt): lane l holds
+// row l & 31, bytes 0-15 = k 16h .. 16h + 15 and bytes 16-31 = k 32 + 16h .. of the 64-k step
+// (h = l >> 5): two ds_read_b128 per fragment, chunks 4kk + h and 4kk + 2 + h of the 128-B row
+// (conflict-free under the bf16 image's c ^ ((r >> 1) & 7)).  Scales: E8M0 bytes of row l & 31,
+// block 2kk + h; a stage pair (256 k) is one dwordx2 per row, loaded by asm beside the DMAs of the
+// pair's first stage (two steps ahead), retired by the step syncs and copied out by asm after
+// them (the compiler does not see the load).  Epilogue: 32 x 32 blocks -> the 16 x 16 fragment
+// layout through the wave's 8 KiB of LDS, 32 rows at a time, then the bf16 kernels' finish256
+// or the MXFP8 output epilogue on each 128 x 64 half.
+constexpr int W8_PAIR = 256;  // k per scale load (8 E8M0 bytes per row)
+
+__device__ __forceinline__ void w8_mfma(f32x16& acc, const i32x8& b, const i32x8& a, int sb, int sa) {
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+               : "+a"(acc)
+               : "v"(b), "v"(a), "v"(sb), "v"(sa));
+}
+__device__ __forceinline__ u32x2 w8_scale_load(const SRsrc& r, int voff) {
+  u32x2 v;
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r.v) : "memory");
+  return v;
+}
+// the loaded words, after a vmcnt wait: this lane's byte (block parity h) moved to bit 0 of each
+__device__ __forceinline__ u32x2 w8_scale_take(const u32x2& v, int sh) {
+  u32x2 o;
+  asm volatile("v_lshrrev_b32 %0, %2, %3\n\tv_lshrrev_b32 %1, %2, %4" : "=&v"(o[0]), "=&v"(o[1]) : "v"(sh), "v"(v[0]),
+               "v"(v[1]));
+  return o;
+}
+
+struct W8Lane {
+  int a_rd[2][2], b_rd[2][2];  // [kk][chunk half] byte offsets inside a stage
+};
+__device__ __forceinline__ W8Lane w8_lane(int wm, int wn, int lane) {
+  W8Lane w;
+  const int r = lane & 31, h = lane >> 5, sw = (r >> 1) & 7;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = 4 * kk + 2 * e + h;
+      w.a_rd[kk][e] = (wm * 128 + r) * 128 + ((c ^ sw) << 4);
+      w.b_rd[kk][e] = 32768 + (wn * 128 + r) * 128 + ((c ^ sw) << 4);
+    }
+  return w;
+}
+__device__ __forceinline__ u32x4 w8_rd(const char* p) { return *LDS_PTR(const u32x4, p); }
+
+// this k-step's scale operands from the stage's words (this lane's byte at bit 0 after
+// w8_scale_take): k-step 0 uses byte 0, k-step 1 byte 2; the trailing s_nop 1 covers the "VALU
+// wrote an MFMA source" hazard for the asm MFMAs that follow
+template <int KK>
+__device__ __forceinline__ void w8_kk_scales(const u32x2 (&ca)[4], const u32x2 (&cb)[4], int u, int (&sA)[4],
+                                             int (&sB)[4]) {
+  const int sh = 16 * KK;
+#define W8_S(i)                                                                                                   \
+  asm volatile("v_lshrrev_b32 %0, %2, %3\n\tv_lshrrev_b32 %1, %2, %4" : "=&v"(sA[i]), "=&v"(sB[i]) : "v"(sh), \
+               "v"(u ? ca[i][1] : ca[i][0]), "v"(u ? cb[i][1] : cb[i][0]))
+  W8_S(0);
+  W8_S(1);
+  W8_S(2);
+  W8_S(3);
+#undef W8_S
+  asm volatile("s_nop 1" : "+v"(sA[0]), "+v"(sA[1]), "+v"(sA[2]), "+v"(sA[3]), "+v"(sB[0]), "+v"(sB[1]), "+v"(sB[2]),
+               "+v"(sB[3]));
+}
+
+// One half-step (k-step kk of a stage): 16 MFMAs on the current fragments; after MFMA g the next
+// half-step's read g (16 ds_read_b128 = 8 fragments, from stage rst, k-step nkk) and, with DMA,
+// this wave's DMA piece g of the stage after next.  sA / sB: this k-step's scale operands.
+template <bool READ, bool DMA>
+__device__ __forceinline__ void w8_half(f32x16 (&acc)[4][4], const i32x8 (&fa)[4], const i32x8 (&fb)[4],
+                                        i32x8 (&na)[4], i32x8 (&nb)[4], const int (&sA)[4], const int (&sB)[4],
+                                        const char* rst, int nkk, const W8Lane& w8, const W4Lane& w, int wave,
+                                        char* dimg, const SRsrc& ra, const SRsrc& rb, int lda2, int ldb2) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int i = g >> 2, j = g & 3;
+    w8_mfma(acc[i][j], fb[j], fa[i], sB[j], sA[i]);
+    if (READ) {
+      const int f = (g & 7) >> 1, e = g & 1;
+      const u32x4 v = w8_rd(rst + (g < 8 ? w8.a_rd[nkk][e] : w8.b_rd[nkk][e]) + f * 4096);
+      i32x8& d = g < 8 ? na[f] : nb[f];
+      d[4 * e] = (int)v[0];
+      d[4 * e + 1] = (int)v[1];
+      d[4 * e + 2] = (int)v[2];
+      d[4 * e + 3] = (int)v[3];
+    }
+    if (DMA) {
+      if (g == 0) w4_piece<true, true>(dimg, 0, ra, w.a_dma, lda2, wave, 0);
+      else if (g < 8) w4_piece<true>(dimg, 0, ra, w.a_dma, lda2, wave, g);
+      else w4_piece<true>(dimg, 32768, rb, w.b_dma, ldb2, wave, g - 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+
+template <typename OutT, int EPI>
+__global__ __launch_bounds__(W4_THR, 1) void gemm_w4p8_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = gridDim.x, nitems = p.ntiles;
+  int item = xcd_remap(blockIdx.x, nwg);
+  if (item >= nitems) return;
+  // the fp8 buffers addressed as bf16 pairs: a 128-k fp8 stage is a 64-element bf16 stage
+  GemmP q = p;
+  q.lda = p.lda / 2;
+  q.ldb = p.ldb / 2;
+  const int lda2 = (int)q.lda, ldb2 = (int)q.ldb;
+  const int K2 = p.K / 2, ns = p.K / 128, kb = p.K / 32;
+  const W4Lane w = w4_lane<true, true>(wave, lane, q.lda, q.ldb);
+  const W8Lane w8 = w8_lane(wm, wn, lane);
+  const int h = lane >> 5, hsh = 8 * h;
+  const SRsrc rsa = make_srsrc(p.a_scale, (uint32_t)((int64_t)p.M * kb));  // rows past M read 0
+  const SRsrc rsb = make_srsrc(p.b_scale, (uint32_t)((int64_t)p.N * kb));
+  auto coords = [&](int it, int& m0, int& n0) {
+    int tm, tn;
+    tile_coords(p, it, tm, tn);
+    m0 = tm * BT;
+    n0 = tn * BT;
+  };
+  // this lane's scale rows: A blocks wm*128 + 32i + (l & 31), B blocks wn*128 + 32j + (l & 31)
+  auto load_scales = [&](int m0, int n0, int pair, u32x2 (&sa)[4], u32x2 (&sb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sa[i] = w8_scale_load(rsa, ((m0 + wm * 128 + 32 * i + (lane & 31)) * kb + 8 * pair));
+      sb[i] = w8_scale_load(rsb, ((n0 + wn * 128 + 32 * i + (lane & 31)) * kb + 8 * pair));
+    }
+  };
+  auto prologue = [&](int it) {  // stages 0, 1 of item it
+    int m0, n0;
+    coords(it, m0, n0);
+    w4_stage_dma<true, true>(smem, q, w, wave, m0, n0, 0, K2, true);
+    w4_stage_dma<true, true>(smem + W4_STAGE, q, w, wave, m0, n0, 64, K2, ns > 1);
+  };
+  u32x2 nsa[4], nsb[4];  // in flight: the next scale pair
+  prologue(item);
+  f32x16 acc[4][4];
+  i32x8 a0[4], b0[4], a1[4], b1[4];
+  const SRsrc none = SRsrc{u32x4{0u, 0u, 0u, 0u}};
+  while (true) {
+    int m0, n0;
+    coords(item, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    load_scales(m0, n0, 0, nsa, nsb);  // scale pair 0 (not held across the previous epilogue: registers)
+    w4_sync();  // stages 0, 1 and scale pair 0 landed (every wave); the previous epilogue's LDS rows consumed
+    u32x2 csa[4], csb[4];  // the current scale pair, this lane's bytes at bit 0 of each word's low byte
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      csa[i] = w8_scale_take(nsa[i], hsh);
+      csb[i] = w8_scale_take(nsb[i], hsh);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const u32x4 va = w8_rd(smem + w8.a_rd[0][e] + f * 4096), vb = w8_rd(smem + w8.b_rd[0][e] + f * 4096);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a0[f][4 * e + r] = (int)va[r];
+          b0[f][4 * e + r] = (int)vb[r];
+        }
+      }
+    // two stages per iteration (ns is even: K % 256 == 0), so the scale word of a stage is static
+#pragma unroll 1
+    for (int s = 0; s < ns; s += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int st = s + u;
+        char* img = smem + u * W4_STAGE;  // stage st lives in slot st & 1 = u
+        char* nxt = smem + (u ^ 1) * W4_STAGE;
+        if (u == 0 && s >= 2) {  // pair s / 2 (loaded beside stage s's DMAs) landed at stage s - 1's sync
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            csa[i] = w8_scale_take(nsa[i], hsh);
+            csb[i] = w8_scale_take(nsb[i], hsh);
+          }
+        }
+        int sA[4], sB[4];
+        w8_kk_scales<0>(csa, csb, u, sA, sB);
+        w8_half<true, false>(acc, a0, b0, a1, b1, sA, sB, img, 1, w8, w, wave, nullptr, none, none, 0, 0);
+        w4_sync();
+        w8_kk_scales<1>(csa, csb, u, sA, sB);
+        const bool more = st + 2 < ns;
+        const SRsrc ra = w4_rsrc<true>((const bf16*)p.A, q.lda, m0, p.M, (st + 2) * 64, K2, more);
+        const SRsrc rb = w4_rsrc<true>((const bf16*)p.B, q.ldb, n0, p.N, (st + 2) * 64, K2, more);
+        w8_half<true, true>(acc, a1, b1, a0, b0, sA, sB, nxt, 0, w8, w, wave, img, ra, rb, lda2, ldb2);
+        if (u == 0 && st + 2 < ns) load_scales(m0, n0, (st + 2) / 2, nsa, nsb);  // pair of stages st + 2, st + 3
+      }
+    }
+    w4_mfma_drain();
+    const int next = item + nwg;
+    if (next < nitems) prologue(next);
+    // epilogue: per 32 x 64 block pair (a, b = 2c, 2c + 1) -> the 16 x 16 fragment layout through
+    // this wave's 8 KiB of LDS, then the 16-B-store epilogue on those 32 rows.  (A direct epilogue
+    // from the 32 x 32 layout -- permlane32 pairing, bf16 rows staged through LDS per unit -- measured
+    // 20-25 % slower per launch: profiles/r04_fp8_gemm.log.)
+    char* st_w = smem + 2 * W4_STAGE + wave * 8192;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        f32x4 acc16[2][4];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int r = lane & 31, cc = 8 * b2 + 2 * qq + h;
+            const f32x16& v = acc[a][2 * c + b2];
+            *LDS_PTR(f32x4, st_w + r * 256 + ((cc ^ (r & 15)) << 4)) =
+                f32x4{v[4 * qq], v[4 * qq + 1], v[4 * qq + 2], v[4 * qq + 3]};
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 16 * i2 + (lane & 15), cc = 4 * j + (lane >> 4);
+            acc16[i2][j] = *LDS_PTR(const f32x4, st_w + r * 256 + ((cc ^ (r & 15)) << 4));
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int mb = m0 + wm * 128 + 32 * a, nb = n0 + wn * 128 + 64 * c;
+        if constexpr (std::is_same<OutT, uint8_t>::value) {
+          epilogue_q8<EPI, 2>(p, acc16, mb, nb, lane);
+        } else if constexpr (std::is_same<OutT, float>::value) {  // fp32 output: per-fragment generic stores
+#pragma unroll
+          for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int m = mb + 16 * i2 + (lane & 15), n = nb + 16 * j + (lane >> 4) * 4;
+              float v[4] = {acc16[i2][j][0], acc16[i2][j][1], acc16[i2][j][2], acc16[i2][j][3]};
+              if (m < p.M && n < p.N) epilogue4<float, EPI>(p, m, n, v);
+            }
+        } else {
+          epilogue256_w<EPI < 0 ? 0 : EPI, false, 2>(p, acc16, mb, nb, lane);
+        }
+      }
+    if (next >= nitems) break;
+    item = next;
+  }
+}
+
+template <typename OutT, int EPI>
+void launch_w4p8(const GemmP& p, hipStream_t s) {
+  constexpr int L = 2 * W4_STAGE + 4 * 8192;
+  (void)lds_optin((const void*)gemm_w4p8_kernel<OutT, EPI>, L);
+  GemmP q = p;
+  q.tiles_n = (p.N + BT - 1) / BT;
+  q.ntiles = q.tiles_n * ((p.M + BT - 1) / BT);
+  const int grid = std::min(q.ntiles, num_cus_w4());
+  hipLaunchKernelGGL((gemm_w4p8_kernel<OutT, EPI>), dim3(grid), dim3(W4_THR), L, s, q);
+}
 }  // namespace
 
 // forward (k-major B) and dgrad (row-major-in-k B) products with bf16 output and one of the
@@ -529,9 +870,38 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
 
 // weight gradients (both operands row-major in k, fp32 output): split-K slabs (p.ws) or the
 // beta epilogue (one split), with the fused bias gradient when bg != nullptr
+// MXFP8 forward products on the persistent 4-wave kernel: K % 256 == 0 (whole scale pairs) and at
+// least one full tile; nullptr leaves them to gemm.hip's 8-wave fp8 kernel
+// Production: long-K products (fc2, K = 4096: 1.48 vs 1.87 ms at L/14@336 B = 512) and bias-only
+// outputs (qkv: 1.41 vs 1.50 ms); the residual / activation epilogues at K = 1024 measured equal or
+// 5 % slower than the 8-wave kernel (its non-persistent workgroups spread the epilogue stores over
+// time; profiles/r04_fp8_gemm.log).  41: this kernel for every covered shape (tests, A/B).
+const char* dispatch_w4_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, int flags) {
+  if (p.K % W8_PAIR != 0 || p.M < BT || p.N < BT || p.var == 40) return nullptr;  // 40: the 8-wave kernel (A/B)
+  if (p.var != 41 && !(p.K >= 2048 || (flags == CLIPMI_EPI_BIAS && !q8o && !f32o))) return nullptr;
+  constexpr int B8 = CLIPMI_EPI_BIAS, Q8 = CLIPMI_EPI_QGELU, R8 = CLIPMI_EPI_RESID;
+  if (q8o) {
+    if (flags != (B8 | Q8)) return nullptr;
+    launch_w4p8<uint8_t, B8 | Q8>(p, s);
+    return "gemm_fp8_fwd_bias_qgelu_q8";
+  }
+  if (f32o) {
+    launch_w4p8<float, -1>(p, s);
+    return "gemm_fp8";
+  }
+  if (!p.vec8) return nullptr;  // the 16-B-store epilogue needs aligned bf16 rows
+  switch (flags) {
+    case B8: launch_w4p8<bf16, B8>(p, s); return "gemm_fp8_fwd_bias";
+    case B8 | R8: launch_w4p8<bf16, B8 | R8>(p, s); return "gemm_fp8_fwd_bias_resid";
+    case B8 | Q8: launch_w4p8<bf16, B8 | Q8>(p, s); return "gemm_fp8_fwd_bias_qgelu";
+    case 0: launch_w4p8<bf16, 0>(p, s); return "gemm_fp8";
+    default: return nullptr;
+  }
+}
+
 const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg) {
   if (p.ws) {
-    if (p.var == 31) {
+    if (p.var == 32) {  // L2 prefetch of both operands (measured 5-8 % slower on the CLIP shapes)
       if (bg) launch_w4p<false, false, float, 0, true, true>(p, splits, s, bg);
       else launch_w4p<false, false, float, 0, false, true>(p, splits, s, bg);
       return "gemm256_wgrad_splitk";

@@ -388,8 +388,8 @@ __device__ __forceinline__ void store8(bf16* p, const float v[8]) {
 // row-group q = lane>>4 holds 8 consecutive columns, fragment 2jp + (q & 1), columns
 // 8*(q >> 1) .. +7, so every residual/aux load and every store is one 16-B access covering
 // 16 rows x 64 B per instruction: half the memory instructions for the same bytes.
-template <int EPI, bool AR = false>
-__device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+template <int EPI, bool AR = false, int NI = 8>
+__device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[NI][4], int mb, int nb, int lane) {
   constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
   constexpr bool HR = EPI & CLIPMI_EPI_RESID, HDQ = EPI & CLIPMI_EPI_DQGELU, HDG = EPI & CLIPMI_EPI_DGELU;
   constexpr bool HBETA = EPI & CLIPMI_EPI_BETA, HPRE = EPI & CLIPMI_EPI_STORE_PRE;
@@ -411,13 +411,14 @@ __device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4]
       }
     }
   }
+  constexpr int NH = NI >= 4 ? NI / 4 : 1, NII = NI >= 4 ? 4 : NI;  // row fragments in groups of <= 4
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float xin[4][2][8];
+  for (int h = 0; h < NH; ++h) {
+    float xin[NII][2][8];
     if (HR || HAUX || HBETA) {
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+      for (int ii = 0; ii < NII; ++ii) {
+        const int m = min(mb + (h * NII + ii) * 16 + mlane, p.M - 1);
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
           const int n = min(nb + 32 * jp + coff, p.N - 8);
@@ -428,8 +429,8 @@ __device__ __forceinline__ void epilogue256_w(const GemmP& p, f32x4 (&acc)[8][4]
       }
     }
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = h * 4 + ii;
+    for (int ii = 0; ii < NII; ++ii) {
+      const int i = h * NII + ii;
       const int m = mb + i * 16 + mlane;
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
@@ -796,9 +797,73 @@ __device__ __forceinline__ void finish256x2(const GemmP& p, f32x4 (&acc)[2][8][4
   finish256<OutT, EPI, AR>(p, acc[1], mb, nb + 64, lane, kz, stage);
 }
 
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// MXFP8 output (fc1 -> fc2 in the fp8 towers): alpha, bias, activation, then per 32-column
+// block of a row -- the 8-column pieces of lanes mlane + 16q, q = 0..3 (epilogue256_lds's
+// permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3 bytes (8 B per lane).
+template <int EPI, int NI = 8>
+__device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4], int mb, int nb, int lane) {
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);
+  uint8_t* out = (uint8_t*)p.C;
+  const int nsb = p.N >> 5;
+  float bv[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const int n = min(nb + 32 * jp + coff, p.N - 8);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) {
+        load4((const float*)p.bias + n, bv[jp]);
+        load4((const float*)p.bias + n + 4, bv[jp] + 4);
+      } else {
+        load8((const bf16*)p.bias + n, bv[jp]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int m = mb + i * 16 + mlane;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int n = nb + 32 * jp + coff;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+        v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
+        v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+      }
+      float am = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if (HQ) v[r] = quick_gelu(v[r]);
+        if (HG) v[r] = gelu_erf(v[r]);
+        am = fmaxf(am, fabsf(v[r]));
+      }
+      am = fmaxf(am, __shfl_xor(am, 16, 64));
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const int ex = mx_exponent(am);
+      const float inv = ldexpf(1.0f, -ex);
+      const uint32_t w0 = mx_pack4(v[0], v[1], v[2], v[3], inv), w1 = mx_pack4(v[4], v[5], v[6], v[7], inv);
+      if (m < p.M && n < p.N) {
+        *(u32x2*)(out + (int64_t)m * p.ldc + n) = u32x2{w0, w1};
+        if (q == 0) p.c_scale[(int64_t)m * nsb + ((nb + 32 * jp) >> 5)] = (uint8_t)(ex + 127);
+      }
+    }
+  }
+}
+
 // 4-wave 256x256 kernel (gemm4.hip) for the forward / dgrad layouts; nullptr if not covered
 const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int dm);
 // its persistent weight-gradient form (both operands row-major in k, fp32 out, split-K slabs)
 const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg);
+// its MXFP8 form (gemm4.hip gemm_w4p8_kernel); nullptr if the shape or epilogue is not covered
+const char* dispatch_w4_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, int flags);
 
 }  // namespace cmg
