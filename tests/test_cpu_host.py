@@ -89,6 +89,32 @@ def test_epilogue_flag_without_operand_is_rejected(flag, operand):
     assert operand.encode()[:3] in _lib.lib().clipmi_last_error()
 
 
+@pytest.mark.parametrize("case", ["D", "A", "ln_w", "saved", "ws"])
+def test_adapter_bad_arguments_rejected(case):
+    """clipmi_adapter_fwd / _bwd reject D or A not a multiple of 8, ln without its weights, a
+    partial set of saved tensors and a short backward workspace with CLIPMI_ERR_INVALID before any
+    launch (pointers here are never dereferenced)."""
+    from clipmi import _lib
+    from clipmi import towers as T  # noqa: F401  (declares the prototypes)
+    L = _lib.lib()
+    p = 4096
+    R, D, A = 4, 512, 64
+    if case == "ws":
+        need = L.clipmi_adapter_bwd_ws(R, D, A)
+        assert need == (R * (D + A) + 1 * (3 * D + A)) * 4
+        st = L.clipmi_adapter_bwd(None, 0, R, D, A, p, D, p, D, p, p, p, p, p, p, p, p, 1, p, D, *([None] * 6), p,
+                                  need - 4)
+    else:
+        if case == "D":
+            D = 510
+        if case == "A":
+            A = 60
+        lnw = None if case == "ln_w" else p
+        act = None if case == "saved" else p
+        st = L.clipmi_adapter_fwd(None, 0, R, D, A, p, D, p, p, p, p, lnw, p, 1e-5, 1, p, D, p, act, p, p, p)
+    assert st == -1, case
+
+
 @pytest.mark.parametrize("combo", [("EPI_STORE_PRE", "EPI_STORE_DACT"), ("EPI_MUL_AUX", "EPI_RESID"),
                                    ("EPI_MUL_AUX", "EPI_BETA"), ("EPI_DQGELU", "EPI_STORE_PRE"),
                                    ("EPI_MUL_AUX", "EPI_DQGELU")])

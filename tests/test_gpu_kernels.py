@@ -435,13 +435,19 @@ def test_im2col_uint8_matches_processor(golden, tag, dtype, P):
     assert (X.float() - Xr.float()).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("tag,D,ln", [("text", 512, True), ("vision", 768, True), ("textual", 512, False)])
-def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln):
+def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln, fused, monkeypatch):
     """towers.AdapterFn on every token of [2, 5, D] (TextAdapter / VisionAdapter, and with ln=False
     peclip.TextualAdapter, adapter/peclip.py:13-18) through libclipmi: output, input gradient and
-    parameter gradients vs the reference modules' run (tests/golden/adapters.npz)."""
+    parameter gradients vs the reference modules' run (tests/golden/adapters.npz).  fused: the
+    one-launch clipmi_adapter_fwd / clipmi_adapter_bwd (the pooled-row path); otherwise the GEMM
+    path AdapterFn takes on full hidden states."""
     import types
+    from clipmi import towers as T
+    if not fused:
+        monkeypatch.setattr(T.AdapterFn, "FUSED_MAX_ROWS", 0)
     import numpy as np
     from clipmi import synth
     from clipmi import towers as T
@@ -469,6 +475,67 @@ def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln):
     assert rel(x.grad.float().cpu().numpy(), g[f"{tag}_gx"]) < tol
     for k, p in mod.named_parameters():
         assert rel(p.grad.cpu().numpy(), g[f"{tag}_g/{k}"]) < (tol if precision == "fp32" else 0.1), k
+
+
+def _adapter_torch(x, sd, ln):
+    """fp32 PyTorch restatement of TextAdapter.forward (adapter/clip_adapter.py:17-23)."""
+    import torch.nn.functional as F
+    h = F.gelu(F.linear(x, sd["down.weight"], sd["down.bias"]))
+    z = F.linear(h, sd["up.weight"], sd["up.bias"]) + x
+    return F.layer_norm(z, (x.shape[-1],), sd["ln.weight"], sd["ln.bias"], 1e-5) if ln else z
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("R,D,A,ln", [(1024, 768, 256, True), (1000, 1024, 256, True), (77, 512, 64, False),
+                                      (1, 512, 256, True)])
+def test_adapter_fused_pooled_rows_matches_torch(dtype, R, D, A, ln):
+    """clipmi_adapter_fwd / clipmi_adapter_bwd at the pooled-row sizes of the bench configs (R = the
+    per-GPU batch, ragged R = 1000, a single row) vs an fp32 PyTorch autograd run of the same
+    adapter on the same (storage-dtype-rounded) inputs; parameter gradients accumulate onto
+    non-zero grads; a replay is bitwise equal (fixed-order sums).  Tolerance: max-relative 2e-5
+    fp32, 3e-2 bf16 (storage rounding of pre / act / z)."""
+    g = torch.Generator().manual_seed(R + D + A)
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).cuda().to(dtype)
+    sd = {"down.weight": mk(A, D, sc=D ** -0.5), "down.bias": mk(A, sc=0.1), "up.weight": mk(D, A, sc=A ** -0.5),
+          "up.bias": mk(D, sc=0.1), "ln.weight": mk(D, sc=0.2) + 1, "ln.bias": mk(D, sc=0.1)}
+    x, dy = mk(R, D), mk(R, D)
+    names = ["down.weight", "down.bias", "up.weight", "up.bias", "ln.weight", "ln.bias"]
+    grads0 = {k: torch.randn(v.shape, generator=g).cuda() for k, v in sd.items()}
+    dc, s = DT[dtype], kern.stream()
+
+    def run():
+        y = torch.empty(R, D, dtype=dtype, device="cuda")
+        pre, act = (torch.empty(R, A, dtype=dtype, device="cuda") for _ in range(2))
+        z = torch.empty(R, D, dtype=dtype, device="cuda")
+        st = torch.empty(2, R, device="cuda")
+        T.call("clipmi_adapter_fwd", s, dc, R, D, A, x.data_ptr(), D, *(sd[k].data_ptr() for k in names), 1e-5,
+               int(ln), y.data_ptr(), D, pre.data_ptr(), act.data_ptr(), z.data_ptr(), st[0].data_ptr(),
+               st[1].data_ptr())
+        gr = {k: v.clone() for k, v in grads0.items()}
+        dx = torch.empty(R, D, dtype=dtype, device="cuda")
+        ws = T._ws(T._lib.lib().clipmi_adapter_bwd_ws(R, D, A), "cuda")
+        T.call("clipmi_adapter_bwd", s, dc, R, D, A, dy.data_ptr(), D, x.data_ptr(), D, pre.data_ptr(),
+               act.data_ptr(), z.data_ptr(), st[0].data_ptr(), st[1].data_ptr(), sd["down.weight"].data_ptr(),
+               sd["up.weight"].data_ptr(), sd["ln.weight"].data_ptr(), int(ln), dx.data_ptr(), D,
+               *(gr[k].data_ptr() for k in names), ws.data_ptr(), ws.numel())
+        torch.cuda.synchronize()
+        return y, dx, gr
+
+    y, dx, gr = run()
+    y2, dx2, gr2 = run()
+    assert torch.equal(y, y2) and torch.equal(dx, dx2) and all(torch.equal(gr[k], gr2[k]) for k in names)
+    ref = {k: v.float().clone().requires_grad_(True) for k, v in sd.items()}
+    xr = x.float().clone().requires_grad_(True)
+    yr = _adapter_torch(xr, ref, ln)
+    yr.backward(dy.float())
+    tol = 2e-5 if dtype == torch.float32 else 3e-2
+    assert rel(y, yr) < tol, "y"
+    assert rel(dx, xr.grad) < tol, "dx"
+    for k in names:
+        if not ln and k.startswith("ln."):
+            assert torch.equal(gr[k], grads0[k]), k  # untouched without the LayerNorm
+            continue
+        assert rel(gr[k] - grads0[k], ref[k].grad) < (tol if dtype == torch.float32 else 5e-2), k
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

@@ -118,6 +118,12 @@ def resize_uint8(images, out_h, out_w):
     return out
 
 
+_lib.declare("clipmi_adapter_fwd", [c_vp, c_int, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_float, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp])
+_lib.declare("clipmi_adapter_bwd_ws", [c_int, c_int, c_int], c_i64)
+_lib.declare("clipmi_adapter_bwd", [c_vp, c_int, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_i64])
 _lib.declare("clipmi_pool_index", [c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp])
 _lib.declare("clipmi_gather_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp])
 _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int])
@@ -509,7 +515,20 @@ class TextTowerFn(torch.autograd.Function):
 
 # ------------------------------------------------------------------------------ adapter
 class AdapterFn(torch.autograd.Function):
-    """y = LN(up(gelu(down(x))) + x)  (ln=False: up(gelu(down(x))) + x)."""
+    """y = LN(up(gelu(down(x))) + x)  (ln=False: up(gelu(down(x))) + x).
+
+    On the pooled rows (R <= FUSED_MAX_ROWS, the training path: model.py runs the adapter on the
+    token-0 / EOS row only) the whole adapter is clipmi_adapter_fwd (one launch) and its backward
+    clipmi_adapter_bwd (two); on full hidden states (text_hidden_states / vision_hidden_states, R =
+    B * S) the same math runs as two GEMMs with fused epilogues + the LayerNorm kernel, whose
+    weight operands are then re-used across many more rows."""
+
+    FUSED_MAX_ROWS = 4096
+
+    @staticmethod
+    def _fused(mod, R):
+        Dh, A = mod.hidden, mod.bottleneck
+        return 0 < R <= AdapterFn.FUSED_MAX_ROWS and Dh % 8 == 0 and A % 8 == 0 and 32 * (2 * Dh + A) <= 160 * 1024
 
     @staticmethod
     def forward(ctx, x, anchor, runtime, mod, need):
@@ -523,24 +542,37 @@ class AdapterFn(torch.autograd.Function):
         dc = dcode(dtype)
         wbuf = _wbuf(arena, dtype)
         dn, up = mod.names
+        fused = AdapterFn._fused(mod, R)
         pre = torch.empty(R, A, dtype=dtype, device=dev) if need else None
-        act = torch.empty(R, A, dtype=dtype, device=dev)
-        flags = _lib.EPI_BIAS | _lib.EPI_GELU | (_lib.EPI_STORE_PRE if need else 0)
-        K.gemm(R, A, Dh, x2, Dh, True, arena.view(f"{dn}.weight", wbuf), Dh, True, act, A,
-               bias=arena.view(f"{dn}.bias", wbuf), aux=pre, ldaux=A, flags=flags)
-        z = torch.empty(R, Dh, dtype=dtype, device=dev)
-        K.gemm(R, Dh, A, act, A, True, arena.view(f"{up}.weight", wbuf), A, True, z, Dh,
-               bias=arena.view(f"{up}.bias", wbuf), residual=x2, ldr=Dh, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
-        if mod.has_ln:
+        if fused:
             y = torch.empty(R, Dh, dtype=dtype, device=dev)
-            stats = torch.empty(2, R, dtype=torch.float32, device=dev)
-            call("clipmi_layernorm_fwd", s, dc, P_(z), Dh, P_(y), Dh, arena.ptr("layer_norm.weight", wbuf),
-                 arena.ptr("layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, Dh, 1e-5, None, None, 0)
+            act = torch.empty(R, A, dtype=dtype, device=dev) if need else None
+            z = torch.empty(R, Dh, dtype=dtype, device=dev) if need and mod.has_ln else None
+            stats = torch.empty(2, R, dtype=torch.float32, device=dev) if need and mod.has_ln else None
+            ln_ptr = (lambda n: arena.ptr(n, wbuf)) if mod.has_ln else (lambda n: None)
+            call("clipmi_adapter_fwd", s, dc, R, Dh, A, P_(x2), Dh, arena.ptr(f"{dn}.weight", wbuf),
+                 arena.ptr(f"{dn}.bias", wbuf), arena.ptr(f"{up}.weight", wbuf), arena.ptr(f"{up}.bias", wbuf),
+                 ln_ptr("layer_norm.weight"), ln_ptr("layer_norm.bias"), 1e-5, int(mod.has_ln), P_(y), Dh, P_(pre),
+                 P_(act), P_(z), P_(stats[0]) if stats is not None else None,
+                 P_(stats[1]) if stats is not None else None)
         else:
-            y, stats = z, None
+            act = torch.empty(R, A, dtype=dtype, device=dev)
+            flags = _lib.EPI_BIAS | _lib.EPI_GELU | (_lib.EPI_STORE_PRE if need else 0)
+            K.gemm(R, A, Dh, x2, Dh, True, arena.view(f"{dn}.weight", wbuf), Dh, True, act, A,
+                   bias=arena.view(f"{dn}.bias", wbuf), aux=pre, ldaux=A, flags=flags)
+            z = torch.empty(R, Dh, dtype=dtype, device=dev)
+            K.gemm(R, Dh, A, act, A, True, arena.view(f"{up}.weight", wbuf), A, True, z, Dh,
+                   bias=arena.view(f"{up}.bias", wbuf), residual=x2, ldr=Dh, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
+            if mod.has_ln:
+                y = torch.empty(R, Dh, dtype=dtype, device=dev)
+                stats = torch.empty(2, R, dtype=torch.float32, device=dev)
+                call("clipmi_layernorm_fwd", s, dc, P_(z), Dh, P_(y), Dh, arena.ptr("layer_norm.weight", wbuf),
+                     arena.ptr("layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, Dh, 1e-5, None, None, 0)
+            else:
+                y, stats = z, None
         if need:
             ctx.save = (x2, pre, act, z, stats)
-            ctx.mod, ctx.rt, ctx.shape = mod, runtime, shp
+            ctx.mod, ctx.rt, ctx.shape, ctx.fused = mod, runtime, shp, fused
         return y.view(shp)
 
     @staticmethod
@@ -560,6 +592,19 @@ class AdapterFn(torch.autograd.Function):
         wbuf = _wbuf(arena, dtype)
         dn, up = mod.names
         dy2 = dy.to(dtype).reshape(R, Dh).contiguous()
+        dx = torch.empty(R, Dh, dtype=dtype, device=dev)
+        if ctx.fused:
+            gp = (lambda n: arena.ptr(n, g)) if train_params else (lambda n: None)
+            lnp = gp if mod.has_ln else (lambda n: None)
+            ws = _ws(_lib.lib().clipmi_adapter_bwd_ws(R, Dh, A), dev)
+            call("clipmi_adapter_bwd", s, dc, R, Dh, A, P_(dy2), Dh, P_(x2), Dh, P_(pre), P_(act), P_(z),
+                 P_(stats[0]) if stats is not None else None, P_(stats[1]) if stats is not None else None,
+                 arena.ptr(f"{dn}.weight", wbuf), arena.ptr(f"{up}.weight", wbuf),
+                 arena.ptr("layer_norm.weight", wbuf) if mod.has_ln else None, int(mod.has_ln), P_(dx), Dh,
+                 gp(f"{dn}.weight"), gp(f"{dn}.bias"), gp(f"{up}.weight"), gp(f"{up}.bias"),
+                 lnp("layer_norm.weight"), lnp("layer_norm.bias"), P_(ws), ws.numel())
+            ctx.save = None
+            return dx.view(ctx.shape), None, None, None, None
         if mod.has_ln:
             dz = torch.empty(R, Dh, dtype=dtype, device=dev)
             lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, Dh), dev)
@@ -584,7 +629,6 @@ class AdapterFn(torch.autograd.Function):
                    bias_grad=arena.view(f"{dn}.bias", g) if bf else None)
             if not bf:
                 call("clipmi_colsum", s, dc, P_(dpre), A, R, A, arena.ptr(f"{dn}.bias", g), 1, P_(cws), cws.numel())
-        dx = torch.empty(R, Dh, dtype=dtype, device=dev)
         K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
                flags=_lib.EPI_RESID)
         ctx.save = None  # released with backward (see VisionTowerFn)
