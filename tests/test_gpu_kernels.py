@@ -230,8 +230,9 @@ def test_text_embedding_fwd_bwd(dtype):
 @pytest.mark.parametrize("B,N,H,causal", [(4, 197, 12, False), (3, 150, 2, True), (2, 224, 3, False),
                                            (2, 129, 2, False), (2, 255, 2, False)])
 def test_attention_wave_count_invariant(B, N, H, causal, monkeypatch):
-    """The 16-wave whole-K/V kernels (one query / key block per wave) compute every block with the
-    same instruction sequence as the 8-wave ones (two blocks per wave): identical outputs."""
+    """The 16-wave whole-K/V kernels (one query / key block per wave) and the 4-wave backward (four
+    blocks per wave, non-causal 128 < N <= 224) compute every block with the same instruction
+    sequence as the 8-wave ones (two blocks per wave): identical outputs."""
     D = H * 64
     qkv = rnd((B * N, 3 * D), 21, torch.bfloat16)
     do = rnd((B * N, D), 22, torch.bfloat16)
@@ -244,7 +245,7 @@ def test_attention_wave_count_invariant(B, N, H, causal, monkeypatch):
     s = kern.stream()
     monkeypatch.setenv("CLIPMI_ATTN_FA", "0")
     outs = []
-    for nw in ("8", "16"):
+    for nw in ("8", "16", "4"):
         monkeypatch.setenv("CLIPMI_ATTN_FWD_NW", nw)
         monkeypatch.setenv("CLIPMI_ATTN_BWD_NW", nw)
         o = torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda")
@@ -256,8 +257,9 @@ def test_attention_wave_count_invariant(B, N, H, causal, monkeypatch):
                do.data_ptr(), dqkv.data_ptr(), mp, int(causal), B, H, N, D)
         torch.cuda.synchronize()
         outs.append((o, lse, dqkv))
-    for a, b, nm in zip(outs[0], outs[1], ("O", "lse", "dqkv")):
-        assert torch.equal(a, b), nm
+    for other in outs[1:]:
+        for a, b, nm in zip(outs[0], other, ("O", "lse", "dqkv")):
+            assert torch.equal(a, b), nm
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

@@ -72,7 +72,22 @@ struct AttnP {
   const bf16* dout; bf16* dqkv;
   int B, H, N, D;
   float scale;
+  unsigned long long* dbg = nullptr;  // diagnostic builds only (CLIPMI_ATTN_STAMPS): s_memtime stamps
 };
+
+// Diagnostic build (-DCLIPMI_ATTN_STAMPS, tools/attn_stamps.py): the prefetching backward stamps
+// s_memtime per (workgroup < 256, wave, item < 16) at the phase boundaries of its item loop into the
+// buffer armed by clipmi_gemm_stamps: [((blk * 16 + wave) * 16 + item) * 8 + phase].
+#ifdef CLIPMI_ATTN_STAMPS
+namespace cmg { unsigned long long* gemm_stamp_buffer(); }
+#define ATT_ST(ph)                                                                                   \
+  do {                                                                                               \
+    if (p.dbg && blockIdx.x < 256 && it < 16 && lane == 0)                                           \
+      p.dbg[((blockIdx.x * 16 + wave) * 16 + it) * 8 + (ph)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+#else
+#define ATT_ST(ph) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------- fwd, prefetching
 // Persistent forward.  (A first version ran one (batch, head) per workgroup with K/V
@@ -604,16 +619,17 @@ struct BwdCtx {
 
 // dK, dV of the wave's NB key blocks (kb = wave, wave + NW): K/V fragments in registers,
 // Q/dO images in LDS.
-template <bool CAUSAL, int NB, bool LOWREG = false>
-__device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[2][2], const bf16x8 (&vf)[2][2],
+template <bool CAUSAL, int NB, bool LOWREG = false, int NBA>
+__device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[NBA][2], const bf16x8 (&vf)[NBA][2],
                                             int wave, int NW) {
+  static_assert(NB <= NBA, "bwd_phase_a: fragments");
   const int lane = c.lane, g = lane >> 4, li = lane & 15;
   bool kok[NB];
   int key[NB];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     key[u] = (wave + NW * u) * 16 + li;
-    kok[u] = c.keyok[key[u]];
+    kok[u] = key[u] < c.N ? c.keyok[key[u]] != 0 : false;  // blocks past N (4-wave form) read nothing
   }
   f32x4 dv[NB][4], dk[NB][4];
 #pragma unroll
@@ -686,17 +702,19 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
 
 // dQ of the wave's NB query blocks (qb = wave, wave + NW): Q/dO fragments in registers, K/V
 // images in LDS; the blocks advance together over the keys, sharing every K/V read.
-template <bool CAUSAL, int NB, bool LOWREG = false>
-__device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[2][2], const bf16x8 (&of)[2][2],
+template <bool CAUSAL, int NB, bool LOWREG = false, int NBA>
+__device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[NBA][2], const bf16x8 (&of)[NBA][2],
                                             int wave, int NW) {
+  static_assert(NB <= NBA, "bwd_phase_b: fragments");
   const int lane = c.lane, g = lane >> 4, li = lane & 15;
   int q[NB];
   float l2[NB], dl[NB];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     q[u] = (wave + NW * u) * 16 + li;
-    l2[u] = c.lse2[q[u]];
-    dl[u] = c.delta[q[u]];
+    const int qi = min(q[u], c.NPAD - 1);  // blocks past NPAD (4-wave form): never stored
+    l2[u] = c.lse2[qi];
+    dl[u] = c.delta[qi];
   }
   f32x4 dq[NB][4];
 #pragma unroll
@@ -758,12 +776,15 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
   }
 }
 
-template <bool CAUSAL, int NW>
+template <bool CAUSAL, int NW, int NBM>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   constexpr int NT = NW * 64;
-  // key / query blocks per wave: two with 8 waves (N <= 256), one with 16 (N <= 256: 4 waves per
-  // SIMD, 128 registers each, so one wave's MFMA -> exp -> MFMA chain hides behind three others)
-  constexpr int NBM = NW >= 16 ? 1 : 2;
+  // key / query blocks per wave (NBM): two with 8 waves (N <= 256) or 4 waves (N <= 128); one with
+  // 16 (N <= 256: 4 waves per SIMD, 128 registers each, so one wave's MFMA -> exp -> MFMA chain
+  // hides behind three others); four with 4 waves (N <= 256, non-causal: one wave per SIMD whose
+  // four blocks share every Q / dO / K / V fragment read, halving the LDS traffic of the 8-wave form)
+  static_assert(NBM == 4 ? (NW == 4 && !CAUSAL) : NBM == (NW >= 16 ? 1 : 2), "attn_bwd_pf: blocks per wave");
+  constexpr int NBA = NBM < 2 ? 2 : NBM;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -809,7 +830,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
       dma16(rv, Vimg + j * 1024, r * (int)ld * 2 + c);
     }
   };
-  auto load_kvfrag = [&](int item, bf16x8 (&kf)[2][2], bf16x8 (&vf)[2][2]) {
+  auto load_kvfrag = [&](int item, bf16x8 (&kf)[NBA][2], bf16x8 (&vf)[NBA][2]) {
     const bf16* base = qkv_of(item);
 #pragma unroll
     for (int u = 0; u < NBM; ++u) {
@@ -838,7 +859,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   };
 
   int item = blockIdx.x;
-  bf16x8 kf[2][2], vf[2][2];
+  bf16x8 kf[NBA][2], vf[NBA][2];
   {
     float l2v;
     int kov;
@@ -852,8 +873,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     const float* lse2 = arr + sl * 3 * NPAD;
     float* delta = arr + sl * 3 * NPAD + NPAD;
     const int* keyok = (const int*)(arr + sl * 3 * NPAD + 2 * NPAD);
+    ATT_ST(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // Q/dO/O(i), meta(i) ready; K/V images free
+    ATT_ST(1);
     const int cur = item, nxt = item + gridDim.x;
     const int b = cur / H, h = cur - b * H;
     const BwdCtx c{Qimg, dOimg, Kimg, Vimg, lse2, delta, keyok, p.dqkv + (int64_t)b * N * ld + h * 64, ld,
@@ -872,11 +895,14 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     }
     raw_barrier_lds();
     issue_kv(cur);
+    ATT_ST(2);
 
     // ---- phase A: dK, dV (Q image, dO image); a wave with two key blocks advances them
     // together so each Q/dO fragment read from LDS feeds both
     // (causal: blocks far apart need different query ranges, so they run one at a time)
-    if constexpr (NBM == 1) {
+    if constexpr (NBM == 4) {
+      bwd_phase_a<CAUSAL, 4>(c, kf, vf, wave, NW);  // blocks past N compute P = 0 and store nothing
+    } else if constexpr (NBM == 1) {
       if (wave < nkb) bwd_phase_a<CAUSAL, 1, true>(c, kf, vf, wave, NW);
     } else if (!CAUSAL && wave + NW < nkb) {
       bwd_phase_a<CAUSAL, 2>(c, kf, vf, wave, NW);
@@ -888,8 +914,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
         bwd_phase_a<CAUSAL, 1>(c, kf1, vf1, wave + NW, NW);
       }
     }
+    ATT_ST(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // K/V(i) images landed; phase A's reads of Q/dO done
+    ATT_ST(4);
 
     // ---- phase B: dQ (K image, V image)
     const bool more = nxt < nitems;
@@ -900,7 +928,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
       load_meta(nxt, l2n, kon);
     }
     const int nqb = (N + 15) >> 4;
-    bf16x8 qf[2][2], of[2][2];
+    bf16x8 qf[NBA][2], of[NBA][2];
 #pragma unroll
     for (int u = 0; u < NBM; ++u) {
       const int q = min((wave + NW * u) * 16, NPAD - 16) + li;
@@ -912,7 +940,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     }
     raw_barrier_lds();  // every wave holds its Q/dO fragments: the images may be overwritten
     if (more) issue_qdo(nxt);
-    if constexpr (NBM == 1) {
+    ATT_ST(5);
+    if constexpr (NBM == 4) {
+      bwd_phase_b<CAUSAL, 4>(c, qf, of, wave, NW);
+    } else if constexpr (NBM == 1) {
       if (wave < nqb) bwd_phase_b<CAUSAL, 1, true>(c, qf, of, wave, NW);
     } else if (!CAUSAL && wave + NW < nqb) {
       bwd_phase_b<CAUSAL, 2>(c, qf, of, wave, NW);
@@ -924,6 +955,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
         bwd_phase_b<CAUSAL, 1>(c, qf1, of1, wave + NW, NW);
       }
     }
+    ATT_ST(6);
     if (!more) break;
     store_meta(sl ^ 1, l2n, kon);  // slot sl ^ 1's readers (item i - 1) finished long ago
     item = nxt;
@@ -1660,15 +1692,15 @@ int fwd_dispatch(const AttnP& p, int causal, hipStream_t s) {
 }
 
 
-template <bool C, int NW>
+template <bool C, int NW, int NBM = (NW >= 16 ? 1 : 2)>
 void launch_bwd_pf(const AttnP& p, hipStream_t s) {
   const int npad = (p.N + 31) & ~31;
   const size_t lds = 5 * (size_t)npad * 128 + 6 * (size_t)npad * 4;
-  (void)lds_optin((const void*)attn_bwd_pf<C, NW>, 160 * 1024);
+  (void)lds_optin((const void*)attn_bwd_pf<C, NW, NBM>, 160 * 1024);
   const int nitems = p.B * p.H;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
   const int grid = std::min(nitems, 256 * per_cu);
-  hipLaunchKernelGGL((attn_bwd_pf<C, NW>), dim3(grid), dim3(NW * 64), lds, s, p, nitems);
+  hipLaunchKernelGGL((attn_bwd_pf<C, NW, NBM>), dim3(grid), dim3(NW * 64), lds, s, p, nitems);
 }
 template <bool C, int NW, int NKC>
 void launch_bwd_sp(const AttnP& p, hipStream_t s) {
@@ -1710,7 +1742,9 @@ int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
   // two blocks per wave share and one block per wave does not
   const char* e = getenv("CLIPMI_ATTN_BWD_NW");
   const int nw = e ? atoi(e) : 8;
-  if (p.N <= 128) {
+  if (nw == 4 && !causal && p.N > 128 && p.N <= 224) {  // 4 waves x 4 blocks (NPAD <= 256 threads)
+    launch_bwd_pf<false, 4, 4>(p, s);
+  } else if (p.N <= 128) {
     if (causal) launch_bwd_pf<true, 4>(p, s); else launch_bwd_pf<false, 4>(p, s);
   } else if (nw == 16 && p.N <= 256) {
     if (causal) launch_bwd_pf<true, 16>(p, s); else launch_bwd_pf<false, 16>(p, s);
@@ -1764,6 +1798,9 @@ extern "C" int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, co
   if (B == 0) return CLIPMI_OK;
   if (dtype == CLIPMI_BF16) {
     AttnP p{(const bf16*)qkv, (bf16*)o, (float*)lse, attention_mask, (const bf16*)dout, (bf16*)dqkv, B, H, N, D, 0.125f};
+#ifdef CLIPMI_ATTN_STAMPS
+    p.dbg = cmg::gemm_stamp_buffer();
+#endif
     const int npad = (N + 31) & ~31;
     size_t lds = (size_t)npad * 128 * 2 + (size_t)npad * 12;
     CLIPMI_HIP(lds_optin((const void*)attn_bwd_mfma<true>, 160 * 1024));
