@@ -26,6 +26,10 @@
 #include <algorithm>
 #include <cstdlib>
 
+#ifdef CLIPMI_ATTN_STAMPS
+namespace cmg { unsigned long long* gemm_stamp_buffer(); }
+#endif
+
 namespace {
 
 constexpr int ATTN_MAX_N = 288;      // whole-K/V-in-LDS kernels (bf16)
@@ -79,7 +83,6 @@ struct AttnP {
 // s_memtime per (workgroup < 256, wave, item < 16) at the phase boundaries of its item loop into the
 // buffer armed by clipmi_gemm_stamps: [((blk * 16 + wave) * 16 + item) * 8 + phase].
 #ifdef CLIPMI_ATTN_STAMPS
-namespace cmg { unsigned long long* gemm_stamp_buffer(); }
 #define ATT_ST(ph)                                                                                   \
   do {                                                                                               \
     if (p.dbg && blockIdx.x < 256 && it < 16 && lane == 0)                                           \
@@ -1380,14 +1383,17 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
         }
       }
       float mt = NEG_INF;
+      const bool tail = k0 + FA_KT > N;  // wave-uniform: only the last tile holds keys past N
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
+        if (MASKED || tail) {  // unmasked: no per-element test on the other tiles
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + st * 16 + 4 * g + r;
-          bool ok = key < N;
-          if (MASKED) ok = ok && keyok[key] && (!causal || key <= qrow[u]);
-          if (!ok) sc[st][r] = NEG_INF;
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + st * 16 + 4 * g + r;
+            bool ok = key < N;
+            if (MASKED) ok = ok && keyok[key] && (!causal || key <= qrow[u]);
+            if (!ok) sc[st][r] = NEG_INF;
+          }
         }
         mt = fmaxf(mt, fmaxf(fmaxf(sc[st][0], sc[st][1]), fmaxf(sc[st][2], sc[st][3])));
       }
@@ -1396,14 +1402,19 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
       const float mt2 = mt * c2;
       // deferred maximum: move the offset only when this tile's max exceeds it by > FA_THR
       if constexpr (!MASKED) {  // every tile holds a valid key: mt2 finite; the row's 4 lanes agree
+        // the rescale only when some row of the wave moved its offset (a wave-uniform branch: the
+        // deferred maximum leaves it untaken on most tiles; 867-893 -> 809-832 us at L/14@336,
+        // profiles/r04_attn_fwd_ab.log)
         const float mn = mt2 > m[u] + FA_THR ? fmaxf(m[u], mt2) : m[u];
-        const float f = __builtin_amdgcn_exp2f(m[u] - mn);  // 1 unmoved, 0 on the first tile
+        if (__builtin_amdgcn_read_exec() && __any(mn != m[u])) {
+          const float f = __builtin_amdgcn_exp2f(m[u] - mn);  // 1 unmoved, 0 on the first tile
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
+          for (int v = 0; v < 4; ++v)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
+            for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+          for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+        }
         m[u] = mn;
       } else if (__builtin_amdgcn_read_exec() && __any(mt2 > m[u] + FA_THR)) {
         const float mn = fmaxf(m[u], mt2);
