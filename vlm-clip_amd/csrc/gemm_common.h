@@ -800,9 +800,13 @@ __device__ __forceinline__ void finish256x2(const GemmP& p, f32x4 (&acc)[2][8][4
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-// MXFP8 output (fc1 -> fc2 in the fp8 towers): alpha, bias, activation, then per 32-column
-// block of a row -- the 8-column pieces of lanes mlane + 16q, q = 0..3 (epilogue256_lds's
-// permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3 bytes (8 B per lane).
+// MXFP8 output (fc1 -> fc2 in the fp8 towers) of a wave's NI*16 x 64 block in the 16x16 fragment
+// layout: alpha, bias, activation, then per 32-column block of a row -- the 8-column pieces of lanes
+// mlane + 16q, q = 0..3 (the permlane16_swap pairing) -- the shared max, its E8M0 scale and the e4m3
+// bytes.  The two 8-B pieces a lane quantised (columns coff .. + 7 of the two 32-column blocks) are
+// exchanged with lane l ^ 32 (v_permlane32_swap) so each lane holds 16 contiguous bytes of its row --
+// lanes q = 0..3 columns 16 q .. 16 q + 15, a whole 64-B row segment per 4 lanes: half the store
+// instructions of 8-B pieces -- and the row's two scale bytes go out as one 16-bit store.
 template <int EPI, int NI = 8>
 __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4], int mb, int nb, int lane) {
   constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
@@ -828,9 +832,10 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4],
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int m = mb + i * 16 + mlane;
+    uint32_t w[2][2];
+    int ex[2];
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
-      const int n = nb + 32 * jp + coff;
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -848,12 +853,24 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4],
       }
       am = fmaxf(am, __shfl_xor(am, 16, 64));
       am = fmaxf(am, __shfl_xor(am, 32, 64));
-      const int ex = mx_exponent(am);
-      const float inv = ldexpf(1.0f, -ex);
-      const uint32_t w0 = mx_pack4(v[0], v[1], v[2], v[3], inv), w1 = mx_pack4(v[4], v[5], v[6], v[7], inv);
-      if (m < p.M && n < p.N) {
-        *(u32x2*)(out + (int64_t)m * p.ldc + n) = u32x2{w0, w1};
-        if (q == 0) p.c_scale[(int64_t)m * nsb + ((nb + 32 * jp) >> 5)] = (uint8_t)(ex + 127);
+      ex[jp] = mx_exponent(am);
+      const float inv = ldexpf(1.0f, -ex[jp]);
+      w[jp][0] = mx_pack4(v[0], v[1], v[2], v[3], inv);
+      w[jp][1] = mx_pack4(v[4], v[5], v[6], v[7], inv);
+    }
+    // lanes < 32 keep their block-0 piece and take lane l + 32's; lanes >= 32 take lane l - 32's
+    // block-1 piece and keep their own
+    const auto s0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[1][0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[1][1], false, false);
+    const int col = nb + 16 * q;
+    if (m < p.M && col < p.N) *(u32x4*)(out + (int64_t)m * p.ldc + col) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    if (q == 0 && m < p.M) {
+      const int sb = (nb >> 5);
+      if ((nsb & 1) == 0 && nb + 64 <= p.N) {
+        *(uint16_t*)(p.c_scale + (int64_t)m * nsb + sb) = (uint16_t)((ex[0] + 127) | ((ex[1] + 127) << 8));
+      } else {
+        p.c_scale[(int64_t)m * nsb + sb] = (uint8_t)(ex[0] + 127);
+        if (nb + 32 < p.N) p.c_scale[(int64_t)m * nsb + sb + 1] = (uint8_t)(ex[1] + 127);
       }
     }
   }
