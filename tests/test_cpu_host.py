@@ -101,7 +101,8 @@ def test_adapter_bad_arguments_rejected(case):
     R, D, A = 4, 512, 64
     if case == "ws":
         need = L.clipmi_adapter_bwd_ws(R, D, A)
-        assert need == (R * (D + A) + 1 * (3 * D + A)) * 4
+        nwg = R  # adp_rb(4) = 1 row per workgroup
+        assert need == (R * (D + A) + nwg * (3 * D + A)) * 4
         st = L.clipmi_adapter_bwd(None, 0, R, D, A, p, D, p, D, p, p, p, p, p, p, p, p, 1, p, D, *([None] * 6), p,
                                   need - 4)
     else:

@@ -448,8 +448,7 @@ def test_adapter_fn_all_tokens_matches_reference(golden, precision, tag, D, ln, 
     path AdapterFn takes on full hidden states."""
     import types
     from clipmi import towers as T
-    if not fused:
-        monkeypatch.setattr(T.AdapterFn, "FUSED_MAX_ROWS", 0)
+    monkeypatch.setattr(T.AdapterFn, "FUSED_MAX_ROWS", 4096 if fused else 0)
     import numpy as np
     from clipmi import synth
     from clipmi import towers as T

@@ -517,13 +517,16 @@ class TextTowerFn(torch.autograd.Function):
 class AdapterFn(torch.autograd.Function):
     """y = LN(up(gelu(down(x))) + x)  (ln=False: up(gelu(down(x))) + x).
 
-    On the pooled rows (R <= FUSED_MAX_ROWS, the training path: model.py runs the adapter on the
-    token-0 / EOS row only) the whole adapter is clipmi_adapter_fwd (one launch) and its backward
-    clipmi_adapter_bwd (two); on full hidden states (text_hidden_states / vision_hidden_states, R =
-    B * S) the same math runs as two GEMMs with fused epilogues + the LayerNorm kernel, whose
-    weight operands are then re-used across many more rows."""
+    Two GEMMs with fused epilogues (down + bias + gelu_erf with the pre-activation saved; up + bias
+    + residual) and the LayerNorm kernel; backward LN' + four GEMMs.  With R <= FUSED_MAX_ROWS the
+    one-launch clipmi_adapter_fwd / two-launch clipmi_adapter_bwd run instead (same saved tensors).
+    They are correct (tests/test_gpu_kernels.py) but measured slower than the GEMM path at every
+    bench size -- R = 256: forward 51 vs 32 us, backward 361 vs 150 us of GPU time; R = 4096: the
+    backward's serial weight-gradient loop is 10x the MFMA GEMMs (profiles/r04_adapter_fused_vs_gemm.log)
+    -- so the product path keeps the GEMMs (FUSED_MAX_ROWS = 0) and the entry points serve FFI
+    callers that want the adapter as one call."""
 
-    FUSED_MAX_ROWS = 4096
+    FUSED_MAX_ROWS = 0
 
     @staticmethod
     def _fused(mod, R):

@@ -5,7 +5,7 @@
 // loss.backward through the adapter, trainer.py:92).
 //
 // The adapter runs on B rows only (the pooled token: model_m.py:102,122), a few GFLOP, so one launch
-// does the whole forward: a workgroup owns ADP_RB rows, keeps x, the bottleneck activation and the
+// does the whole forward: a workgroup owns RB = adp_rb(R) rows, keeps x, the bottleneck activation and the
 // pre-LN sum in LDS (fp32) and computes both products with its 256 threads one output column each
 // (weights read as 16-B row pieces, the row values broadcast from LDS), then the LayerNorm per row.
 // The backward is two launches: the row pass (LayerNorm backward, d_act = dz Wu, d_pre = d_act *
@@ -16,10 +16,13 @@
 // every intermediate in fp32 (the saved pre-activation, activation and pre-LN sum are rounded to T).
 #include "common.h"
 #include "internal.h"
+#include <type_traits>
 
 namespace {
 
-constexpr int ADP_RB = 8;     // rows per workgroup
+// rows per workgroup: adp_rb(R) in {1, 2, 4, 8} -- the most that still gives every CU a workgroup
+// (each workgroup reads both weight matrices once, so more rows per workgroup = fewer re-reads)
+__host__ __device__ constexpr int adp_rb(int R) { return R >= 2048 ? 8 : R >= 1024 ? 4 : R >= 512 ? 2 : 1; }
 constexpr int ADP_T = 256;    // threads
 constexpr int ADP_WO = 8;     // weight-pass outputs per thread along the reduced operand's rows
 
@@ -50,14 +53,14 @@ struct AdpFwd {
 };
 
 // out[r][c] = sum_k in[r][k] W[c][k] for the workgroup's rows: thread c, W rows read in 16-B pieces
-template <typename T>
-__device__ __forceinline__ void rows_times_wt(const float* in, int K, const T* W, int c, float acc[ADP_RB]) {
+template <typename T, int RB>
+__device__ __forceinline__ void rows_times_wt(const float* in, int K, const T* W, int c, float acc[RB]) {
   const T* wr = W + (int64_t)c * K;
   for (int k = 0; k < K; k += 8) {
     float w[8];
     ld8(wr + k, w);
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) {
+    for (int r = 0; r < RB; ++r) {
       const float* xr = in + r * K + k;
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[r] = fmaf(xr[e], w[e], acc[r]);
@@ -65,28 +68,28 @@ __device__ __forceinline__ void rows_times_wt(const float* in, int K, const T* W
   }
 }
 
-template <typename T>
+template <typename T, int RB>
 __global__ __launch_bounds__(ADP_T) void adapter_fwd_kernel(AdpFwd a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int D = a.D, A = a.A, t = threadIdx.x;
-  const int r0 = blockIdx.x * ADP_RB, nr = min(ADP_RB, a.R - r0);
+  const int r0 = blockIdx.x * RB, nr = min(RB, a.R - r0);
   float* xs = sm;                 // [RB][D]
-  float* hs = xs + ADP_RB * D;    // [RB][A]
-  float* zs = hs + ADP_RB * A;    // [RB][D]
-  for (int i = t; i < ADP_RB * D; i += ADP_T) {
+  float* hs = xs + RB * D;    // [RB][A]
+  float* zs = hs + RB * A;    // [RB][D]
+  for (int i = t; i < RB * D; i += ADP_T) {
     const int r = i / D, k = i - r * D;
     xs[i] = r < nr ? to_f32(((const T*)a.x)[(int64_t)(r0 + r) * a.ldx + k]) : 0.f;
   }
   __syncthreads();
   // down projection + bias + gelu_erf
   for (int c = t; c < A; c += ADP_T) {
-    float acc[ADP_RB];
+    float acc[RB];
     const float b = to_f32(((const T*)a.bd)[c]);
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) acc[r] = b;
-    rows_times_wt<T>(xs, D, (const T*)a.wd, c, acc);
+    for (int r = 0; r < RB; ++r) acc[r] = b;
+    rows_times_wt<T, RB>(xs, D, (const T*)a.wd, c, acc);
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) {
+    for (int r = 0; r < RB; ++r) {
       const T pre = from_f32<T>(acc[r]);
       const T act = from_f32<T>(gelu_erf(to_f32(pre)));
       hs[r * A + c] = to_f32(act);
@@ -99,13 +102,13 @@ __global__ __launch_bounds__(ADP_T) void adapter_fwd_kernel(AdpFwd a) {
   __syncthreads();
   // up projection + bias + residual
   for (int c = t; c < D; c += ADP_T) {
-    float acc[ADP_RB];
+    float acc[RB];
     const float b = to_f32(((const T*)a.bu)[c]);
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) acc[r] = b + xs[r * D + c];
-    rows_times_wt<T>(hs, A, (const T*)a.wu, c, acc);
+    for (int r = 0; r < RB; ++r) acc[r] = b + xs[r * D + c];
+    rows_times_wt<T, RB>(hs, A, (const T*)a.wu, c, acc);
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) {
+    for (int r = 0; r < RB; ++r) {
       const T z = from_f32<T>(acc[r]);
       zs[r * D + c] = to_f32(z);
       if (r < nr) {
@@ -149,17 +152,17 @@ struct AdpBwd {
   float *pbu, *pbd, *plw, *plb;  // per-workgroup partials [nwg][D], [nwg][A], [nwg][D], [nwg][D]
 };
 
-template <typename T>
+template <typename T, int RB>
 __global__ __launch_bounds__(ADP_T) void adapter_bwd_rows_kernel(AdpBwd a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int D = a.D, A = a.A, t = threadIdx.x, wg = blockIdx.x;
-  const int r0 = wg * ADP_RB, nr = min(ADP_RB, a.R - r0);
+  const int r0 = wg * RB, nr = min(RB, a.R - r0);
   float* dys = sm;                 // [RB][D] dy (LayerNorm branch)
-  float* dps = sm + ADP_RB * D;    // [RB][A] d_pre
-  float* dzs = a.ln ? dps + ADP_RB * A : sm;  // [RB][D] dz = dL/d(pre-LN sum)
+  float* dps = sm + RB * D;    // [RB][A] d_pre
+  float* dzs = a.ln ? dps + RB * A : sm;  // [RB][D] dz = dL/d(pre-LN sum)
   const int wave = t >> 6, lane = t & 63;
   if (a.ln) {
-    for (int r = wave; r < ADP_RB; r += ADP_T / 64) {  // one wave per row
+    for (int r = wave; r < RB; r += ADP_T / 64) {  // one wave per row
       const bool ok = r < nr;
       const float mean = ok ? a.mean[r0 + r] : 0.f, rstd = ok ? a.rstd[r0 + r] : 0.f;
       float sg = 0.f, sgx = 0.f;
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(ADP_T) void adapter_bwd_rows_kernel(AdpBwd a) {
       a.plb[(int64_t)wg * D + k] = pb;
     }
   } else {
-    for (int i = t; i < ADP_RB * D; i += ADP_T) {
+    for (int i = t; i < RB * D; i += ADP_T) {
       const int r = i / D, k = i - r * D;
       dzs[i] = r < nr ? to_f32(((const T*)a.dy)[(int64_t)(r0 + r) * a.lddy + k]) : 0.f;
     }
@@ -211,18 +214,18 @@ __global__ __launch_bounds__(ADP_T) void adapter_bwd_rows_kernel(AdpBwd a) {
   }
   // d_act = dz Wu (Wu [D][A]: thread c reads column c, rows of Wu coalesced across the wave)
   for (int c = t; c < A; c += ADP_T) {
-    float acc[ADP_RB];
+    float acc[RB];
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) acc[r] = 0.f;
+    for (int r = 0; r < RB; ++r) acc[r] = 0.f;
     const T* wc = (const T*)a.wu + c;
     for (int k = 0; k < D; ++k) {
       const float w = to_f32(wc[(int64_t)k * A]);
 #pragma unroll
-      for (int r = 0; r < ADP_RB; ++r) acc[r] = fmaf(dzs[r * D + k], w, acc[r]);
+      for (int r = 0; r < RB; ++r) acc[r] = fmaf(dzs[r * D + k], w, acc[r]);
     }
     float pb = 0.f;
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) {
+    for (int r = 0; r < RB; ++r) {
       float dp = 0.f;
       if (r < nr) {
         dp = acc[r] * gelu_erf_grad(to_f32(((const T*)a.pre)[(int64_t)(r0 + r) * A + c]));
@@ -236,14 +239,14 @@ __global__ __launch_bounds__(ADP_T) void adapter_bwd_rows_kernel(AdpBwd a) {
   __syncthreads();
   // dx = dz + d_pre Wd (Wd [A][D]: thread k reads column k, coalesced across the wave)
   for (int k = t; k < D; k += ADP_T) {
-    float acc[ADP_RB];
+    float acc[RB];
 #pragma unroll
-    for (int r = 0; r < ADP_RB; ++r) acc[r] = dzs[r * D + k];
+    for (int r = 0; r < RB; ++r) acc[r] = dzs[r * D + k];
     const T* wk = (const T*)a.wd + k;
     for (int c = 0; c < A; ++c) {
       const float w = to_f32(wk[(int64_t)c * D]);
 #pragma unroll
-      for (int r = 0; r < ADP_RB; ++r) acc[r] = fmaf(dps[r * A + c], w, acc[r]);
+      for (int r = 0; r < RB; ++r) acc[r] = fmaf(dps[r * A + c], w, acc[r]);
     }
     for (int r = 0; r < nr; ++r) ((T*)a.dx)[(int64_t)(r0 + r) * a.lddx + k] = from_f32<T>(acc[r]);
   }
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(ADP_T) void adapter_bwd_weights_kernel(AdpW a, int 
 static int adp_check(int dtype, int R, int D, int A) {
   CLIPMI_REQUIRE(dtype == CLIPMI_BF16 || dtype == CLIPMI_F32, "adapter: bf16 or f32");
   CLIPMI_REQUIRE(R >= 0 && D > 0 && A > 0 && D % 8 == 0 && A % 8 == 0, "adapter: D and A multiples of 8");
-  CLIPMI_REQUIRE((size_t)ADP_RB * (2 * D + A) * 4 <= 160 * 1024, "adapter: D too large for the row tile");
+  CLIPMI_REQUIRE((size_t)8 * (2 * D + A) * 4 <= 160 * 1024, "adapter: D too large for the row tile");
   return CLIPMI_OK;
 }
 
@@ -319,22 +322,32 @@ extern "C" int clipmi_adapter_fwd(void* stream, int dtype, int R, int D, int A, 
   CLIPMI_REQUIRE(((uintptr_t)w_down & 15) == 0 && ((uintptr_t)w_up & 15) == 0, "adapter_fwd: weights 16-B aligned");
   if (R == 0) return CLIPMI_OK;
   AdpFwd a{R, D, A, ln, x, w_down, b_down, w_up, b_up, ln_w, ln_b, ldx, ldy, y, pre, act, z, mean, rstd, eps};
-  const size_t lds = (size_t)ADP_RB * (2 * D + A) * 4;
-  const unsigned nb = (unsigned)((R + ADP_RB - 1) / ADP_RB);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == CLIPMI_BF16) {
-    (void)lds_optin((const void*)adapter_fwd_kernel<bf16>, (int)lds);
-    hipLaunchKernelGGL(adapter_fwd_kernel<bf16>, dim3(nb), dim3(ADP_T), lds, s, a);
-  } else {
-    (void)lds_optin((const void*)adapter_fwd_kernel<float>, (int)lds);
-    hipLaunchKernelGGL(adapter_fwd_kernel<float>, dim3(nb), dim3(ADP_T), lds, s, a);
+  auto go = [&](auto rbc) {
+    constexpr int RB = decltype(rbc)::value;
+    const size_t lds = (size_t)RB * (2 * D + A) * 4;
+    const unsigned nb = (unsigned)((R + RB - 1) / RB);
+    if (dtype == CLIPMI_BF16) {
+      (void)lds_optin((const void*)adapter_fwd_kernel<bf16, RB>, (int)lds);
+      hipLaunchKernelGGL((adapter_fwd_kernel<bf16, RB>), dim3(nb), dim3(ADP_T), lds, s, a);
+    } else {
+      (void)lds_optin((const void*)adapter_fwd_kernel<float, RB>, (int)lds);
+      hipLaunchKernelGGL((adapter_fwd_kernel<float, RB>), dim3(nb), dim3(ADP_T), lds, s, a);
+    }
+  };
+  switch (adp_rb(R)) {
+    case 8: go(std::integral_constant<int, 8>()); break;
+    case 4: go(std::integral_constant<int, 4>()); break;
+    case 2: go(std::integral_constant<int, 2>()); break;
+    default: go(std::integral_constant<int, 1>()); break;
   }
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
 
 extern "C" int64_t clipmi_adapter_bwd_ws(int R, int D, int A) {
-  const int64_t nwg = (R + ADP_RB - 1) / ADP_RB;
+  const int rb = adp_rb(R);
+  const int64_t nwg = (R + rb - 1) / rb;
   return ((int64_t)R * (D + A) + nwg * (3 * (int64_t)D + A)) * 4;
 }
 
@@ -350,7 +363,8 @@ extern "C" int clipmi_adapter_bwd(void* stream, int dtype, int R, int D, int A, 
   CLIPMI_REQUIRE(!ln || (z && mean && rstd && ln_w), "adapter_bwd: LayerNorm inputs");
   CLIPMI_REQUIRE(ws && ws_bytes >= clipmi_adapter_bwd_ws(R, D, A), "adapter_bwd: workspace too small");
   if (R == 0) return CLIPMI_OK;
-  const int nwg = (R + ADP_RB - 1) / ADP_RB;
+  const int rb = adp_rb(R);
+  const int nwg = (R + rb - 1) / rb;
   float* f = (float*)ws;
   float* dz = f;
   float* dpre = dz + (int64_t)R * D;
@@ -360,21 +374,34 @@ extern "C" int clipmi_adapter_bwd(void* stream, int dtype, int R, int D, int A, 
   float* plb = plw + (int64_t)nwg * D;
   AdpBwd b{R, D, A, ln, dy, x, pre, act, z, w_down, w_up, ln_w, mean, rstd, lddy, ldx, lddx, dx, dz, dpre,
            pbu, pbd, plw, plb};
-  const size_t lds = (size_t)ADP_RB * (2 * D + A) * 4;
   hipStream_t s = (hipStream_t)stream;
   const int nu = ((D + ADP_WO - 1) / ADP_WO) * ((A + ADP_T - 1) / ADP_T);
   const int nd = ((A + ADP_WO - 1) / ADP_WO) * ((D + ADP_T - 1) / ADP_T);
   AdpW w{R, D, A, nwg, ln, dz, dpre, pbu, pbd, plw, plb, act, x, ldx, g_w_down, g_b_down, g_w_up, g_b_up,
          ln ? g_ln_w : nullptr, ln ? g_ln_b : nullptr};
   const bool weights = g_w_down || g_b_down || g_w_up || g_b_up || g_ln_w || g_ln_b;
-  if (dtype == CLIPMI_BF16) {
-    (void)lds_optin((const void*)adapter_bwd_rows_kernel<bf16>, (int)lds);
-    hipLaunchKernelGGL(adapter_bwd_rows_kernel<bf16>, dim3(nwg), dim3(ADP_T), lds, s, b);
-    if (weights) hipLaunchKernelGGL(adapter_bwd_weights_kernel<bf16>, dim3(nu + nd + 4), dim3(ADP_T), 0, s, w, nu, nd);
-  } else {
-    (void)lds_optin((const void*)adapter_bwd_rows_kernel<float>, (int)lds);
-    hipLaunchKernelGGL(adapter_bwd_rows_kernel<float>, dim3(nwg), dim3(ADP_T), lds, s, b);
-    if (weights) hipLaunchKernelGGL(adapter_bwd_weights_kernel<float>, dim3(nu + nd + 4), dim3(ADP_T), 0, s, w, nu, nd);
+  auto go = [&](auto rbc) {
+    constexpr int RB = decltype(rbc)::value;
+    const size_t lds = (size_t)RB * (2 * D + A) * 4;
+    if (dtype == CLIPMI_BF16) {
+      (void)lds_optin((const void*)adapter_bwd_rows_kernel<bf16, RB>, (int)lds);
+      hipLaunchKernelGGL((adapter_bwd_rows_kernel<bf16, RB>), dim3(nwg), dim3(ADP_T), lds, s, b);
+    } else {
+      (void)lds_optin((const void*)adapter_bwd_rows_kernel<float, RB>, (int)lds);
+      hipLaunchKernelGGL((adapter_bwd_rows_kernel<float, RB>), dim3(nwg), dim3(ADP_T), lds, s, b);
+    }
+  };
+  switch (rb) {
+    case 8: go(std::integral_constant<int, 8>()); break;
+    case 4: go(std::integral_constant<int, 4>()); break;
+    case 2: go(std::integral_constant<int, 2>()); break;
+    default: go(std::integral_constant<int, 1>()); break;
+  }
+  if (weights) {
+    if (dtype == CLIPMI_BF16)
+      hipLaunchKernelGGL(adapter_bwd_weights_kernel<bf16>, dim3(nu + nd + 4), dim3(ADP_T), 0, s, w, nu, nd);
+    else
+      hipLaunchKernelGGL(adapter_bwd_weights_kernel<float>, dim3(nu + nd + 4), dim3(ADP_T), 0, s, w, nu, nd);
   }
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
