@@ -1297,7 +1297,7 @@ __device__ __forceinline__ void fa_stage(char* img, const bf16* col0, int64_t ld
 }
 
 template <int QPW, bool MASKED>
-__global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal, int nqc) {
+__global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal, int nqc, int qbase) {
   constexpr int QC = FA_W * QPW * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qimg = smem;
@@ -1310,7 +1310,7 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
   const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the chunks of one (b, h) share an XCD's L2
   const int bh = wid / nqc, qc = wid - bh * nqc;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = qc * QC;
+  const int q0 = qbase + qc * QC;
   const int nkt = (N + FA_KT - 1) / FA_KT;
   const bf16* base = p.qkv + (int64_t)b * N * ld + h * 64;
   const float c2 = p.scale * LOG2E;
@@ -1463,13 +1463,13 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
 }
 
 template <int QPW, bool M>
-void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s) {
+void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s, int qbase = 0, int nq = -1) {
   constexpr int QC = FA_W * QPW * 16;
   const int nkt = (p.N + FA_KT - 1) / FA_KT;
   const size_t lds = (size_t)QC * 128 + FA_S * FA_TILE + (M ? (size_t)nkt * FA_KT * 4 : 0);
   (void)lds_optin((const void*)attn_fwd_fa<QPW, M>, 160 * 1024);
-  const int nqc = (p.N + QC - 1) / QC;
-  hipLaunchKernelGGL((attn_fwd_fa<QPW, M>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc);
+  const int nqc = ((nq < 0 ? p.N - qbase : nq) + QC - 1) / QC;
+  hipLaunchKernelGGL((attn_fwd_fa<QPW, M>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc, qbase);
 }
 
 int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
@@ -1477,7 +1477,14 @@ int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
   const char* e = getenv("CLIPMI_FA_QPW");  // A/B hook (read per call): 2|4 forces the chunk size
   const int env_qpw = e ? atoi(e) : 0;
   const int qpw = env_qpw == 2 || env_qpw == 4 ? env_qpw : (p.N > 256 ? 4 : 2);
-  if (qpw == 4) {  // 256-query chunks: K/V streamed once per 256 queries
+  if (qpw == 4 && !masked && p.N % 256 != 0 && p.N > 256) {
+    // unmasked: the whole 256-query chunks in one launch and the remainder in 128-query chunks, so
+    // the straight-line block loop computes 640 query rows for N = 577 instead of 768 (L/14@336:
+    // 820 -> 776 us; profiles/r04_attn_fwd_ab.log)
+    const int full = p.N / 256 * 256;
+    launch_fwd_fa<4, false>(p, causal, s, 0, full);
+    launch_fwd_fa<2, false>(p, causal, s, full, p.N - full);
+  } else if (qpw == 4) {  // 256-query chunks: K/V streamed once per 256 queries
     if (masked) launch_fwd_fa<4, true>(p, causal, s); else launch_fwd_fa<4, false>(p, causal, s);
   } else {
     if (masked) launch_fwd_fa<2, true>(p, causal, s); else launch_fwd_fa<2, false>(p, causal, s);
