@@ -807,6 +807,12 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 // exchanged with lane l ^ 32 (v_permlane32_swap) so each lane holds 16 contiguous bytes of its row --
 // lanes q = 0..3 columns 16 q .. 16 q + 15, a whole 64-B row segment per 4 lanes: half the store
 // instructions of 8-B pieces -- and the row's two scale bytes go out as one 16-bit store.
+__device__ __forceinline__ uint32_t mx_pack4_unclamped(float a, float b, float c, float d, float inv) {
+  int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false);
+  pk = __builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, pk, true);
+  return (uint32_t)pk;
+}
+
 template <int EPI, int NI = 8>
 __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4], int mb, int nb, int lane) {
   constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
@@ -855,8 +861,10 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4],
       am = fmaxf(am, __shfl_xor(am, 32, 64));
       ex[jp] = mx_exponent(am);
       const float inv = ldexpf(1.0f, -ex[jp]);
-      w[jp][0] = mx_pack4(v[0], v[1], v[2], v[3], inv);
-      w[jp][1] = mx_pack4(v[4], v[5], v[6], v[7], inv);
+      // no clamp: the block's scale makes |v * inv| <= 448 (e4m3's largest normal) exactly, so
+      // the round-to-nearest-even conversion cannot leave the range for finite v
+      w[jp][0] = mx_pack4_unclamped(v[0], v[1], v[2], v[3], inv);
+      w[jp][1] = mx_pack4_unclamped(v[4], v[5], v[6], v[7], inv);
     }
     // lanes < 32 keep their block-0 piece and take lane l + 32's; lanes >= 32 take lane l - 32's
     // block-1 piece and keep their own
