@@ -95,8 +95,8 @@ FAMILIES = {
 }
 # HBM traffic per launch of each family, from rocprofv3 --pmc passes (tools/traffic_pmc.sh); named
 # explicitly so the file read is the one committed for this build, not the newest on disk
-TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r03_traffic_fwd_dgrad.json",
-                 "gemm256_wgrad": "profiles/r03_traffic_wgrad.json",
+TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r04_traffic_fwd_dgrad.json",
+                 "gemm256_wgrad": "profiles/r04_traffic_wgrad.json",
                  "attention": "profiles/r02_traffic_attention.json"}
 
 
