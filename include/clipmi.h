@@ -189,6 +189,11 @@ int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx
  * attention_mask: int64 [B, N] key padding (1 keep) or NULL; causal for the text tower. */
 int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse, const int64_t* attention_mask,
                          int causal, int B, int H, int N, int D);
+/* The K/V-streaming forward with O written as MXFP8 (OCP e4m3 o8 [B*N, D] + E8M0 s8 [B*N, D/32],
+ * clipmi_quant_mxfp8's rule applied to the fp32 O): the fp8 towers' out-projection operand without a
+ * bf16 round trip (BASELINE config 5).  bf16 q/k/v. */
+int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t* o8, uint8_t* s8, float* lse,
+                               const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, const void* o, const float* lse, const void* dout,
                          void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 

@@ -539,6 +539,54 @@ def test_adapter_fused_pooled_rows_matches_torch(dtype, R, D, A, ln):
         assert rel(gr[k] - grads0[k], ref[k].grad) < (tol if dtype == torch.float32 else 5e-2), k
 
 
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 4, False), (3, 300, 2, True), (1, 1000, 2, False)])
+def test_attention_fwd_mxfp8_output(B, N, H, causal):
+    """clipmi_attention_fwd_mxfp8 (config 5's out-projection operand straight from the streaming
+    forward) vs the same forward's bf16 output: the same lse bit for bit, every block's E8M0 scale by
+    clipmi_quant_mxfp8's rule (a block max on a power-of-two boundary may land either side after the
+    bf16 rounding of the comparison output) and every element within two e4m3 steps."""
+    from clipmi import kernels as K
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 61, torch.bfloat16)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(62)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    mp = mask.data_ptr() if mask is not None else None
+    s = kern.stream()
+    o = torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    q8 = torch.empty(B * N, D, dtype=torch.uint8, device="cuda")
+    s8 = torch.empty(B * N, D // 32, dtype=torch.uint8, device="cuda")
+    lse8 = torch.empty(B * H * N, device="cuda")
+    import os
+    old = os.environ.get("CLIPMI_ATTN_FA")
+    os.environ["CLIPMI_ATTN_FA"] = "1"  # the same (streaming) kernel for the bf16 comparison
+    try:
+        T.call("clipmi_attention_fwd", s, DT[torch.bfloat16], qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), mp,
+               int(causal), B, H, N, D)
+    finally:
+        if old is None:
+            del os.environ["CLIPMI_ATTN_FA"]
+        else:
+            os.environ["CLIPMI_ATTN_FA"] = old
+    T.call("clipmi_attention_fwd_mxfp8", s, qkv.data_ptr(), q8.data_ptr(), s8.data_ptr(), lse8.data_ptr(), mp,
+           int(causal), B, H, N, D)
+    torch.cuda.synchronize()
+    assert torch.equal(lse, lse8)
+    ref = o.float()
+    R = B * N
+    amax = ref.abs().view(R, D // 32, 32).amax(-1)
+    e = torch.ceil(torch.log2(amax / 448.0)).clamp(-127, 127)
+    same = (s8.to(torch.int32) - 127 == e.to(torch.int32)).float().mean().item()
+    assert same >= 0.99, same
+    d = K.MX8(q8, s8).dequant()
+    step = torch.pow(2.0, (s8.to(torch.float32) - 127) - 9).repeat_interleave(32, 1)
+    err = (d - ref).abs() - (ref.abs() * (2.0 ** -3 + 2.0 ** -7) + 2 * step)
+    assert (err <= 0).all(), err.max().item()
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_attention_online_softmax_rescale(dtype, monkeypatch):
     """cdna_hip_programming.md rule 26: force the deferred-max rescale branch of the streaming

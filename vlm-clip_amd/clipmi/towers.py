@@ -130,6 +130,7 @@ _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_in
 _lib.declare("clipmi_attention_fwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_int])
+_lib.declare("clipmi_attention_fwd_mxfp8", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_l2norm_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int])
 _lib.declare("clipmi_l2norm_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int])
 _lib.declare("clipmi_contrastive_ce_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp])

@@ -77,6 +77,7 @@ struct AttnP {
   int B, H, N, D;
   float scale;
   unsigned long long* dbg = nullptr;  // diagnostic builds only (CLIPMI_ATTN_STAMPS): s_memtime stamps
+  uint8_t *o8 = nullptr, *s8 = nullptr;  // MXFP8 output (attn_fwd_fa<.., Q8>): e4m3 [B*N, D], E8M0 [B*N, D/32]
 };
 
 // Diagnostic build (-DCLIPMI_ATTN_STAMPS, tools/attn_stamps.py): the prefetching backward stamps
@@ -1296,7 +1297,7 @@ __device__ __forceinline__ void fa_stage(char* img, const bf16* col0, int64_t ld
   }
 }
 
-template <int QPW, bool MASKED>
+template <int QPW, bool MASKED, bool Q8 = false>
 __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal, int nqc, int qbase) {
   constexpr int QC = FA_W * QPW * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1449,30 +1450,59 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
   }
 #pragma unroll
   for (int u = 0; u < QPW; ++u) {
-    if (!qv[u] || qrow[u] >= N) continue;
+    if (!qv[u] || qrow[u] >= N) continue;  // whole rows: the four lanes of a row (g) agree
     const float l = accl[u][0];
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    bf16* orow = p.o + ((int64_t)b * N + qrow[u]) * D + h * 64;
+    const int64_t row = (int64_t)b * N + qrow[u];
+    if constexpr (Q8) {
+      // the out-projection's MXFP8 operand straight from fp32 O (clipmi_quant_mxfp8's rule): the
+      // head's two 32-column blocks are v = 0, 1 and v = 2, 3 of the row's four lanes g
+      float w[4][4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float w[4] = {acc[u][v][0] * inv, acc[u][v][1] * inv, acc[u][v][2] * inv, acc[u][v][3] * inv};
-      store4(orow + v * 16 + 4 * g, w);
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[v][r] = acc[u][v][r] * inv;
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        float am = 0.f;
+#pragma unroll
+        for (int v = 2 * blk; v < 2 * blk + 2; ++v)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(w[v][r]));
+        am = fmaxf(am, __shfl_xor(am, 16, 64));
+        am = fmaxf(am, __shfl_xor(am, 32, 64));
+        const int ex = mx_exponent(am);
+        const float sc = ldexpf(1.0f, -ex);
+        uint8_t* q = p.o8 + row * D + h * 64;
+#pragma unroll
+        for (int v = 2 * blk; v < 2 * blk + 2; ++v)
+          *(uint32_t*)(q + v * 16 + 4 * g) = mx_pack4(w[v][0], w[v][1], w[v][2], w[v][3], sc);
+        if (g == 0) p.s8[row * (D >> 5) + 2 * h + blk] = (uint8_t)(ex + 127);
+      }
+    } else {
+      bf16* orow = p.o + row * D + h * 64;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float w[4] = {acc[u][v][0] * inv, acc[u][v][1] * inv, acc[u][v][2] * inv, acc[u][v][3] * inv};
+        store4(orow + v * 16 + 4 * g, w);
+      }
     }
     if (g == 0) p.lse[((int64_t)b * H + h) * N + qrow[u]] = l > 0.f ? (m[u] + __log2f(l)) * LN2 : NEG_INF;
   }
 }
 
-template <int QPW, bool M>
+template <int QPW, bool M, bool Q8 = false>
 void launch_fwd_fa(const AttnP& p, int causal, hipStream_t s, int qbase = 0, int nq = -1) {
   constexpr int QC = FA_W * QPW * 16;
   const int nkt = (p.N + FA_KT - 1) / FA_KT;
   const size_t lds = (size_t)QC * 128 + FA_S * FA_TILE + (M ? (size_t)nkt * FA_KT * 4 : 0);
-  (void)lds_optin((const void*)attn_fwd_fa<QPW, M>, 160 * 1024);
+  (void)lds_optin((const void*)attn_fwd_fa<QPW, M, Q8>, 160 * 1024);
   const int nqc = ((nq < 0 ? p.N - qbase : nq) + QC - 1) / QC;
-  hipLaunchKernelGGL((attn_fwd_fa<QPW, M>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc, qbase);
+  hipLaunchKernelGGL((attn_fwd_fa<QPW, M, Q8>), dim3(p.B * p.H * nqc), dim3(FA_W * 64), lds, s, p, causal, nqc, qbase);
 }
 
-int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
+template <bool Q8>
+int fwd_fa_dispatch_t(const AttnP& p, int causal, hipStream_t s) {
   const bool masked = causal || p.kmask;
   const char* e = getenv("CLIPMI_FA_QPW");  // A/B hook (read per call): 2|4 forces the chunk size
   const int env_qpw = e ? atoi(e) : 0;
@@ -1482,15 +1512,16 @@ int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) {
     // the straight-line block loop computes 640 query rows for N = 577 instead of 768 (L/14@336:
     // 820 -> 776 us; profiles/r04_attn_fwd_ab.log)
     const int full = p.N / 256 * 256;
-    launch_fwd_fa<4, false>(p, causal, s, 0, full);
-    launch_fwd_fa<2, false>(p, causal, s, full, p.N - full);
+    launch_fwd_fa<4, false, Q8>(p, causal, s, 0, full);
+    launch_fwd_fa<2, false, Q8>(p, causal, s, full, p.N - full);
   } else if (qpw == 4) {  // 256-query chunks: K/V streamed once per 256 queries
-    if (masked) launch_fwd_fa<4, true>(p, causal, s); else launch_fwd_fa<4, false>(p, causal, s);
+    if (masked) launch_fwd_fa<4, true, Q8>(p, causal, s); else launch_fwd_fa<4, false, Q8>(p, causal, s);
   } else {
-    if (masked) launch_fwd_fa<2, true>(p, causal, s); else launch_fwd_fa<2, false>(p, causal, s);
+    if (masked) launch_fwd_fa<2, true, Q8>(p, causal, s); else launch_fwd_fa<2, false, Q8>(p, causal, s);
   }
   return CLIPMI_OK;
 }
+int fwd_fa_dispatch(const AttnP& p, int causal, hipStream_t s) { return fwd_fa_dispatch_t<false>(p, causal, s); }
 
 // ------------------------------------------------------------------ f32 SIMT path
 // 4 lanes per row, 16 head dims each.  K/V (or Q/dO) staged in LDS as fp32 [N][64].
@@ -1803,6 +1834,27 @@ extern "C" int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, vo
     CLIPMI_HIP(lds_optin((const void*)attn_fwd_f32, 160 * 1024));
     hipLaunchKernelGGL(attn_fwd_f32, dim3(B * H), dim3(1024), lds, s, p);
   }
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// The flash forward with its output written as MXFP8 (the fp8 towers' out-projection operand): o8
+// e4m3 [B*N, D], s8 E8M0 [B*N, D/32], quantised from the fp32 O by clipmi_quant_mxfp8's rule.
+extern "C" int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t* o8, uint8_t* s8, float* lse,
+                                          const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
+  CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N_ANY, "N must be in [1, 4096]");
+  CLIPMI_REQUIRE(qkv && o8 && s8 && lse, "operands");
+  if (B == 0) return CLIPMI_OK;
+  AttnP p{(const bf16*)qkv, nullptr, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
+  p.o8 = o8;
+  p.s8 = s8;
+  const int npad = (N + 31) & ~31;
+  const double flops = 4.0 * B * H * (double)N * npad * 64;
+  ProfScope ps(s, "attn_fwd", flops);
+  CLIPMI_TRY(fwd_fa_dispatch_t<true>(p, causal, s));
+  ps.finish("attn_fwd", flops);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }

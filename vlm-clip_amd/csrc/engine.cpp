@@ -189,13 +189,20 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
       const clipmi_layer_w8& w8 = d->layers8[l];
       const clipmi_layer_act& a = d->act[l];
       void* x_out = (l + 1 < d->L) ? d->act[l + 1].x_in : d->x_out;
-      // producers write the next GEMM's MXFP8 operand directly (no bf16 round trip), except the
-      // attention output, quantised by its own pass
+      // producers write the next GEMM's MXFP8 operand directly (no bf16 round trip); the attention
+      // output too where the streaming forward runs (N > 288)
       CLIPMI_TRY(clipmi_layernorm_fwd_mxfp8(s, bf, a.x_in, D, qa, sa, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps));
       CLIPMI_TRY(gemm8q(s, R, 3 * D, D, qa, sa, w8.qkv_w, w8.qkv_s, a.qkv, 3 * D, CLIPMI_EPI_BIAS, w.qkv_b, nullptr, 0));
-      CLIPMI_TRY(clipmi_attention_fwd(s, bf, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
-      CLIPMI_TRY(gemm8(s, R, D, D, a.o, D, w8.out_w, w8.out_s, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b,
-                       a.x_in, D, qa, sa));
+      if (d->N > 288) {  // the streaming forward writes the out-projection's MXFP8 operand itself
+        CLIPMI_TRY(clipmi_attention_fwd_mxfp8(s, a.qkv, qa, sa, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N,
+                                              D));
+        CLIPMI_TRY(gemm8q(s, R, D, D, qa, sa, w8.out_w, w8.out_s, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b,
+                          a.x_in, D));
+      } else {  // the whole-K/V kernels (N <= 288) write bf16 O, quantised by its own pass
+        CLIPMI_TRY(clipmi_attention_fwd(s, bf, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+        CLIPMI_TRY(gemm8(s, R, D, D, a.o, D, w8.out_w, w8.out_s, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b,
+                         a.x_in, D, qa, sa));
+      }
       CLIPMI_TRY(clipmi_layernorm_fwd_mxfp8(s, bf, a.h, D, qa, sa, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps));
       CLIPMI_TRY(gemm8q(s, R, F, D, qa, sa, w8.fc1_w, w8.fc1_s, qb, F, CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU, w.fc1_b,
                         nullptr, 0, sb));
