@@ -148,6 +148,24 @@ def adapter(x, a, layer_norm_on=True, eps=1e-5):
     return h
 
 
+def mhsa_residual_ln(x, s, heads, eps=1e-5):
+    """peclip.ContextAdapter / SharedAdapter.forward (adapter/peclip.py:31-34, 45-48):
+    layer_norm(mhsa(x, x, x) + x), nn.MultiheadAttention(batch_first=True) restated: [q|k|v] =
+    in_proj(x), per head softmax(q k^T / sqrt(D / heads)) v, out_proj.  x [B, N, D] or [N, D]."""
+    unb = x.dim() == 2
+    if unb:
+        x = x[None]
+    B, N, D = x.shape
+    hd = D // heads
+    qkv = linear(x, s["mhsa.in_proj_weight"], s["mhsa.in_proj_bias"])
+    q, k, v = (t.reshape(B, N, heads, hd).transpose(1, 2) for t in qkv.split(D, dim=-1))
+    pr = torch.softmax((q @ k.transpose(-1, -2)) * hd ** -0.5, dim=-1)
+    o = (pr @ v).transpose(1, 2).reshape(B, N, D)
+    y = layer_norm(linear(o, s["mhsa.out_proj.weight"], s["mhsa.out_proj.bias"]) + x,
+                   s["layer_norm.weight"], s["layer_norm.bias"], eps)
+    return y[0] if unb else y
+
+
 def shared_adapter(x, img, s, heads=8, keep_p=None, keep_m=None, p=0.1):
     """SharedMHSAttentionAdapter.forward, adapter/clip_adapter.py:100-128, with the image tokens
     img [N_v, D_v] broadcast over the batch (quirk Q3; the reference runs at B=1).

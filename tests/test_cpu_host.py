@@ -373,3 +373,35 @@ def test_bench_self_launches_n_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert sorted((d["rank"], d["world"]) for d in lines) == [(0, 2), (1, 2)]
+
+
+@pytest.mark.parametrize("tag,cls,args", [("context", "ContextAdapter", (128, 2)), ("shared", "SharedAdapter", (96, 2)),
+                                          ("textual", "TextualAdapter", (64, 32))])
+def test_peclip_modules_init_like_reference(golden, tag, cls, args):
+    """clipmi.peclip's constructors draw their parameters from torch's generator in the order
+    nn.Linear / nn.MultiheadAttention do (adapter/peclip.py:8-11, 26-29, 40-43): under the same
+    manual_seed the state dict equals the reference module's (tests/golden/peclip.npz), key for key."""
+    from clipmi import peclip
+    g = golden("peclip.npz")
+    torch.manual_seed(5)
+    mod = getattr(peclip, cls)(*args, device="cpu")
+    sd = mod.state_dict()
+    ref = sorted(k[len(f"init_{tag}/"):] for k in g.files if k.startswith(f"init_{tag}/"))
+    assert sorted(sd) == ref
+    for k in ref:
+        assert np.array_equal(sd[k].numpy(), g[f"init_{tag}/{k}"]), k
+
+
+def test_peclip_argument_errors():
+    """nn.MultiheadAttention's checks (num_heads must divide embed_dim; the input's last dimension)
+    and the precision switch; no CPU fallback for the forward."""
+    from clipmi import peclip
+    with pytest.raises(AssertionError, match="divisible"):
+        peclip.ContextAdapter(100, 3, device="cpu")
+    with pytest.raises(ValueError, match="precision"):
+        peclip.SharedAdapter(64, 1, device="cpu", precision="fp16")
+    m = peclip.ContextAdapter(64, 1, device="cpu")
+    with pytest.raises(AssertionError, match="embedding dimension of 64, but got 32"):
+        m(torch.zeros(2, 3, 32))
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        m(torch.zeros(2, 3, 64))

@@ -360,3 +360,23 @@ def test_resize_oracle_matches_pil():
         img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
         ref = np.asarray(Image.fromarray(img).resize((ow, oh), resample=Image.BICUBIC))
         assert np.array_equal(RR.resize_bicubic(img, oh, ow), ref), (h, w, oh, ow)
+
+
+PECLIP_CASES = [("ctx_n7", 128, 2, (2, 7)), ("ctx_n197", 128, 2, (2, 197)), ("shared_hd48", 192, 4, (2, 9)),
+                ("ctx_unbatched", 128, 2, (11,))]
+
+
+@pytest.mark.parametrize("tag,D,heads,shape", PECLIP_CASES)
+def test_peclip_mhsa_oracle_matches_reference(golden, tag, D, heads, shape):
+    """oracle.mhsa_residual_ln against peclip.ContextAdapter / SharedAdapter run from the reference
+    (tests/golden/peclip.npz, tools/gen_goldens.py gen_peclip): output, input and parameter grads."""
+    g = golden("peclip.npz")
+    s = R.to_torch(synth.mhsa_adapter_state_dict(D, 13, tag), requires_grad=True)
+    x = torch.from_numpy(synth.normal(shape + (D,), 13, f"{tag}/x")).requires_grad_(True)
+    gy = torch.from_numpy(synth.normal(shape + (D,), 13, f"{tag}/gy"))
+    y = R.mhsa_residual_ln(x, s, heads)
+    y.backward(gy)
+    np.testing.assert_allclose(y.detach().numpy(), g[f"{tag}_y"], atol=2e-5, rtol=1e-4)
+    np.testing.assert_allclose(x.grad.numpy(), g[f"{tag}_gx"], atol=2e-5, rtol=1e-4)
+    for k, t in s.items():
+        np.testing.assert_allclose(t.grad.numpy(), g[f"{tag}_g/{k}"], atol=5e-5, rtol=1e-4, err_msg=k)

@@ -99,6 +99,37 @@ def gen_adapters():
     save("adapters.npz", **out)
 
 
+def gen_peclip():
+    """adapter/peclip.py's ContextAdapter / SharedAdapter (self-MHSA + LayerNorm residual, :21-48) and
+    TextualAdapter: (1) the parameters each constructor draws under torch.manual_seed(5) (pins the
+    init order); (2) forward + backward with synthetic parameters (non-zero biases, LN affine off
+    identity) on [B, N, D] inputs: head_dim 64 at N = 7 and N = 197 (the flash attention kernels),
+    head_dim 48 (the general per-head path), and an unbatched [N, D] input."""
+    from adapter.peclip import ContextAdapter, SharedAdapter, TextualAdapter
+    out = {}
+    for tag, cls, args in (("context", ContextAdapter, (128, 2)), ("shared", SharedAdapter, (96, 2)),
+                           ("textual", TextualAdapter, (64, 32))):
+        torch.manual_seed(5)
+        mod = cls(*args)
+        for k, v in mod.state_dict().items():
+            out[f"init_{tag}/{k}"] = v.numpy().copy()
+    for tag, cls, D, nh, shape in (("ctx_n7", ContextAdapter, 128, 2, (2, 7)),
+                                   ("ctx_n197", ContextAdapter, 128, 2, (2, 197)),
+                                   ("shared_hd48", SharedAdapter, 192, 4, (2, 9)),
+                                   ("ctx_unbatched", ContextAdapter, 128, 2, (11,))):
+        mod = cls(D, nh)
+        mod.load_state_dict({k: torch.from_numpy(v) for k, v in synth.mhsa_adapter_state_dict(D, 13, tag).items()})
+        x = torch.from_numpy(synth.normal(shape + (D,), 13, f"{tag}/x")).requires_grad_(True)
+        gy = torch.from_numpy(synth.normal(shape + (D,), 13, f"{tag}/gy"))
+        y = mod(x)
+        y.backward(gy)
+        out[f"{tag}_y"] = y.detach().numpy()
+        out[f"{tag}_gx"] = x.grad.numpy()
+        for k, p in mod.named_parameters():
+            out[f"{tag}_g/{k}"] = p.grad.numpy()
+    save("peclip.npz", **out)
+
+
 def gen_forward(preset, B, tag, adapters=True, grads=False, layer=False, freeze_clip=True):
     cfg = C.resolve(preset)
     ref = build_reference_model(cfg, adapters, adapters, freeze_clip=freeze_clip)

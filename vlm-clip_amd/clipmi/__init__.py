@@ -14,6 +14,9 @@ def __getattr__(name):
     if name == "CLIPTokenizer":  # caption BPE of the input step (dataset.py:152-159)
         from .tokenizer import CLIPTokenizer
         return CLIPTokenizer
+    if name in ("ContextAdapter", "SharedAdapter", "TextualAdapter"):  # adapter/peclip.py's modules
+        from . import peclip
+        return getattr(peclip, name)
     if name in ("CLIPAdapterTrainer", "FusedAdamW"):
         from . import trainer
         return getattr(trainer, name)

@@ -166,6 +166,20 @@ def shared_adapter_state_dict(text_in: int, image_in: int, seed: int, prefix: st
     return sd
 
 
+def mhsa_adapter_state_dict(D: int, seed: int, prefix: str):
+    """peclip.ContextAdapter / SharedAdapter (adapter/peclip.py:21-48) weights: every tensor
+    N(0, 1/D), except the LayerNorm affine: weight 1 + N(0, 0.1), bias N(0, 0.1)."""
+    shapes = [("mhsa.in_proj_weight", (3 * D, D)), ("mhsa.in_proj_bias", (3 * D,)),
+              ("mhsa.out_proj.weight", (D, D)), ("mhsa.out_proj.bias", (D,)),
+              ("layer_norm.weight", (D,)), ("layer_norm.bias", (D,))]
+    sd = OrderedDict()
+    for name, shape in shapes:
+        ln = name.startswith("layer_norm")
+        sd[name] = normal(shape, seed, f"{prefix}/{name}", 0.1 if ln else 1.0 / math.sqrt(D),
+                          1.0 if name == "layer_norm.weight" else 0.0)
+    return sd
+
+
 CLIP_MEAN = np.array([0.48145466, 0.4578275, 0.40821073], dtype=np.float64)
 CLIP_STD = np.array([0.26862954, 0.26130258, 0.27577711], dtype=np.float64)
 
