@@ -40,6 +40,7 @@ from clipmi import config as C  # noqa: E402
 METRIC = "image-text pairs/sec, ViT-B/16 contrastive step, 1/2/4/8 GPUs; MFMA % peak"
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/CU/clk (dense bf16, MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5033.2   # block-scaled f8f6f4 MFMA: 2x the bf16 rate (dense)
+PEAK_FP32_TFLOPS = 157.3   # f32 MFMA (= the f32 vector rate, 1/16 of bf16; MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E peak (MI355X_MICROARCH.md: 8 TB/s spec, ~6.3 achievable)
 
 
@@ -55,9 +56,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: the frozen towers' GEMMs in MXFP8 (BASELINE config 5; needs --mode adapter)")
-    ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES),
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"],
+                    help="fp8: the frozen towers' GEMMs in MXFP8 (BASELINE config 5; needs --mode adapter); "
+                         "fp32: the parity mode (f32 operands end to end), priced against the f32 MFMA peak")
+    ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES) + list(FAMILIES_FP32),
                     help="family reported as `roofline` (default: the one with the most measured time)")
     ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -93,6 +95,8 @@ FAMILIES = {
     "gemm_fp8": ["gemm_fp8_fwd_bias", "gemm_fp8_fwd_bias_resid", "gemm_fp8_fwd_bias_qgelu",
                  "gemm_fp8_fwd_bias_qgelu_q8", "gemm_fp8", "gemm_fp8_generic"],
 }
+FAMILIES_FP32 = {"gemm_f32": ["gemm_f32"]}  # --precision fp32: every GEMM is the f32 kernel
+PEAKS = {"gemm_fp8": PEAK_FP8_TFLOPS, "gemm_f32": PEAK_FP32_TFLOPS}
 # HBM traffic per launch of each family, from rocprofv3 --pmc passes (tools/traffic_pmc.sh); named
 # explicitly so the file read is the one committed for this build, not the newest on disk
 TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r04_traffic_fwd_dgrad.json",
@@ -240,9 +244,9 @@ def family_roofline(name, launches, cfg, B, train):
     tot_ms = sum(m for m, _ in launches)
     tot_fl = sum(f for _, f in launches)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
-    peak = PEAK_FP8_TFLOPS if name == "gemm_fp8" else PEAK_BF16_TFLOPS
+    peak = PEAKS.get(name, PEAK_BF16_TFLOPS)
     alg = algorithmic_bytes(cfg, B, train).get(name)
-    res = {"bound": "mfma", "kernel": name, "labels": FAMILIES[name], "launches": len(launches),
+    res = {"bound": "mfma", "kernel": name, "labels": {**FAMILIES, **FAMILIES_FP32}[name], "launches": len(launches),
            "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
            "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
            "frac": round(ach / peak, 4), "ms_per_step_caller_stream": None,
@@ -331,7 +335,8 @@ def main():
     L.clipmi_prof_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
     L.clipmi_prof_read_labels.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     cap = 16384
-    labels = [lab for fam in FAMILIES.values() for lab in fam]
+    fams = FAMILIES_FP32 if args.precision == "fp32" else FAMILIES
+    labels = [lab for fam in fams.values() for lab in fam]
     _lib.check(L.clipmi_prof_arm(",".join(labels).encode(), cap), "prof_arm")
     # only the caller's stream: the text tower's launches run on a second stream beside the
     # vision tower's kernels (model.py), so their event spans include the other tower's work
@@ -370,14 +375,14 @@ def main():
     value = pairs / elapsed
     fwd = C.forward_flops_per_pair(cfg)
     step_flops_pair = 3 * fwd if not adapters else fwd
-    per_fam = {name: [] for name in FAMILIES}
+    per_fam = {name: [] for name in fams}
     for i in range(n):
         lab = labels[wh[i]]
-        for name, labs in FAMILIES.items():
+        for name, labs in fams.items():
             if lab in labs:
                 per_fam[name].append((ms[i], fl[i]))
     roofs = {}
-    for name in FAMILIES:
+    for name in fams:
         r = family_roofline(name, per_fam[name], cfg, args.batch, not adapters)
         if r is not None:
             r["ms_per_step_caller_stream"] = round(sum(m for m, _ in per_fam[name]) / args.steps, 2)
@@ -391,7 +396,7 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp8 (MXFP8 e4m3 tower GEMMs; bf16 elsewhere)" if args.precision == "fp8" else "bf16",
+        "dtype": {"fp8": "fp8 (MXFP8 e4m3 tower GEMMs; bf16 elsewhere)", "fp32": "fp32"}.get(args.precision, "bf16"),
         "data": f"synthetic: CLIP-normalised U[0,1) {cfg.vision_config.image_size}px pixels + BOS/random-id/EOS captions (77 tok, EOS pad), "
                 "random-init weights",
         "config": {"workload": f"{cfg.name} {'full fine-tune (adapters off)' if not adapters else 'adapter fine-tune'}"
@@ -399,8 +404,8 @@ def main():
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": cfg.vision_config.image_size,
                    "text_len": 77, "parallelism": f"dp{world}"},
-        "mfma_frac_step": round(value * step_flops_pair / (world * (PEAK_FP8_TFLOPS if args.precision == "fp8"
-                                                                      else PEAK_BF16_TFLOPS) * 1e12), 4),
+        "mfma_frac_step": round(value * step_flops_pair / (world * {"fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_FP32_TFLOPS}
+                                                           .get(args.precision, PEAK_BF16_TFLOPS) * 1e12), 4),
         "step_tflops_per_gpu": round(value * step_flops_pair / world / 1e12, 1),
         "loss": round(float(loss.item()), 4),
         "roofline": roofs.get(main_fam) if main_fam else None,
