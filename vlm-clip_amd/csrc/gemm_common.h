@@ -799,6 +799,7 @@ __device__ __forceinline__ void finish256x2(const GemmP& p, f32x4 (&acc)[2][8][4
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 // MXFP8 output (fc1 -> fc2 in the fp8 towers) of a wave's NI*16 x 64 block in the 16x16 fragment
 // layout: alpha, bias, activation, then per 32-column block of a row -- the 8-column pieces of lanes
@@ -807,12 +808,6 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 // exchanged with lane l ^ 32 (v_permlane32_swap) so each lane holds 16 contiguous bytes of its row --
 // lanes q = 0..3 columns 16 q .. 16 q + 15, a whole 64-B row segment per 4 lanes: half the store
 // instructions of 8-B pieces -- and the row's two scale bytes go out as one 16-bit store.
-__device__ __forceinline__ uint32_t mx_pack4_unclamped(float a, float b, float c, float d, float inv) {
-  int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false);
-  pk = __builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, pk, true);
-  return (uint32_t)pk;
-}
-
 template <int EPI, int NI = 8>
 __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4], int mb, int nb, int lane) {
   constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU, HG = EPI & CLIPMI_EPI_GELU;
@@ -842,29 +837,40 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4],
     int ex[2];
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
-      float v[8];
+      // the element math in packed fp32 (v_pk_fma / v_pk_mul / v_pk_add: two elements per issue,
+      // bitwise the scalar ops' results); only the exp2 / rcp transcendentals stay per element
+      f32x2 v2[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
                                                          __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
-        v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
-        v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+        // pairs (r, r + 4): the two 16-column halves the swap returns
+        v2[r] = __builtin_elementwise_fma(f32x2{__uint_as_float(sw[0]), __uint_as_float(sw[1])},
+                                          f32x2{p.alpha, p.alpha}, f32x2{bv[jp][r], bv[jp][r + 4]});
       }
       float am = 0.f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if (HQ) v[r] = quick_gelu(v[r]);
-        if (HG) v[r] = gelu_erf(v[r]);
-        am = fmaxf(am, fabsf(v[r]));
+      for (int r = 0; r < 4; ++r) {
+        if (HQ) {
+          const f32x2 z = v2[r] * f32x2{-1.702f * 1.4426950408889634f, -1.702f * 1.4426950408889634f};
+          const f32x2 d = f32x2{__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])} + f32x2{1.0f, 1.0f};
+          v2[r] = v2[r] * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+        }
+        if (HG) v2[r] = f32x2{gelu_erf(v2[r][0]), gelu_erf(v2[r][1])};
+        am = fmaxf(am, fmaxf(fabsf(v2[r][0]), fabsf(v2[r][1])));
       }
       am = fmaxf(am, __shfl_xor(am, 16, 64));
       am = fmaxf(am, __shfl_xor(am, 32, 64));
       ex[jp] = mx_exponent(am);
       const float inv = ldexpf(1.0f, -ex[jp]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v2[r] = v2[r] * f32x2{inv, inv};
       // no clamp: the block's scale makes |v * inv| <= 448 (e4m3's largest normal) exactly, so
       // the round-to-nearest-even conversion cannot leave the range for finite v
-      w[jp][0] = mx_pack4_unclamped(v[0], v[1], v[2], v[3], inv);
-      w[jp][1] = mx_pack4_unclamped(v[4], v[5], v[6], v[7], inv);
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v2[0][0], v2[1][0], 0, false);
+      w[jp][0] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v2[2][0], v2[3][0], pk, true);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(v2[0][1], v2[1][1], 0, false);
+      w[jp][1] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v2[2][1], v2[3][1], pk, true);
     }
     // lanes < 32 keep their block-0 piece and take lane l + 32's; lanes >= 32 take lane l - 32's
     // block-1 piece and keep their own
