@@ -129,22 +129,25 @@ int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, in
 int clipmi_period_sum(void* stream, int dtype, const void* x, int64_t ldx, int nb, int period, int nt, int D,
                       float* out, int beta);
 
-/* ---- Bottleneck adapter on the pooled rows (adapter/clip_adapter.py:17-23 TextAdapter.forward,
- * :144-150 VisionAdapter.forward; adapter/peclip.py:13-18 TextualAdapter with ln = 0) ----------
- * y = LN(up(gelu_erf(down(x))) + x) * ln_w + ln_b (ln = 0: without the LayerNorm), one launch for
- * R rows (ROWS x D, row strides ldx / ldy): w_down [A, D], b_down [A], w_up [D, A], b_up [D]
- * (nn.Linear layout, activation dtype), math in fp32.  pre / act [R, A], z [R, D] (activation
- * dtype) and mean / rstd [R] (fp32) are saved for the backward (all NULL in inference; z / mean /
- * rstd only with ln).  D % 8 == 0, A % 8 == 0, 32 * (2 D + A) <= 160 KiB.  Intended for the
- * pooled rows (R = batch): the whole adapter costs one launch instead of two GEMMs + a LayerNorm. */
+/* ---- Bottleneck adapter (adapter/clip_adapter.py:17-23 TextAdapter.forward, :144-150
+ * VisionAdapter.forward; adapter/peclip.py:13-18 TextualAdapter with ln = 0) --------------------
+ * y = LN(up(gelu_erf(down(x))) + x) * ln_w + ln_b (ln = 0: without the LayerNorm) for R rows
+ * (row strides ldx / ldy): w_down [A, D], b_down [A], w_up [D, A], b_up [D] (nn.Linear layout,
+ * activation dtype).  One call sequences the library's own kernels on the stream (csrc/adapter.cpp):
+ * down GEMM (+ bias + gelu_erf; pre-activation stored when pre != NULL), up GEMM (+ bias + residual),
+ * LayerNorm -- the path the Python mirror runs.  act [R, A] is required (it carries the bottleneck
+ * between the GEMMs); with ln also z [R, D] (the pre-LN sum) and mean / rstd [R] (fp32).  pre [R, A]
+ * is saved for the backward (NULL in inference).  D % 8 == 0, A % 8 == 0; with ln D % 64 == 0, D <= 1024. */
 int clipmi_adapter_fwd(void* stream, int dtype, int R, int D, int A, const void* x, int64_t ldx, const void* w_down,
                        const void* b_down, const void* w_up, const void* b_up, const void* ln_w, const void* ln_b,
                        float eps, int ln, void* y, int64_t ldy, void* pre, void* act, void* z, float* mean,
                        float* rstd);
 int64_t clipmi_adapter_bwd_ws(int R, int D, int A);
 /* dx = dL/dx given dy = dL/dy (the forward's saved tensors); the fp32 parameter gradients g_*
- * (each may be NULL; g_ln_* ignored when ln = 0) ACCUMULATE (+=, AccumulateGrad), summed in a fixed
- * order (bitwise reproducible).  Two launches: the row pass and the weight pass. */
+ * (each may be NULL; g_ln_* ignored when ln = 0) ACCUMULATE (+=, AccumulateGrad): LN backward, the
+ * up / down weight-gradient GEMMs (bias gradients fused in bf16, a column sum in fp32), the
+ * gelu_erf'-fused input-gradient GEMM and the residual-fused dx GEMM; no atomics across tiles, so a
+ * replay is bitwise equal. */
 int clipmi_adapter_bwd(void* stream, int dtype, int R, int D, int A, const void* dy, int64_t lddy, const void* x,
                        int64_t ldx, const void* pre, const void* act, const void* z, const float* mean,
                        const float* rstd, const void* w_down, const void* w_up, const void* ln_w, int ln, void* dx,

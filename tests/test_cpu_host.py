@@ -92,8 +92,8 @@ def test_epilogue_flag_without_operand_is_rejected(flag, operand):
 @pytest.mark.parametrize("case", ["D", "A", "ln_w", "saved", "ws"])
 def test_adapter_bad_arguments_rejected(case):
     """clipmi_adapter_fwd / _bwd reject D or A not a multiple of 8, ln without its weights, a
-    partial set of saved tensors and a short backward workspace with CLIPMI_ERR_INVALID before any
-    launch (pointers here are never dereferenced)."""
+    missing activation buffer (act carries the bottleneck between the launches) and a short backward
+    workspace with CLIPMI_ERR_INVALID before any launch (pointers here are never dereferenced)."""
     from clipmi import _lib
     from clipmi import towers as T  # noqa: F401  (declares the prototypes)
     L = _lib.lib()
@@ -101,8 +101,7 @@ def test_adapter_bad_arguments_rejected(case):
     R, D, A = 4, 512, 64
     if case == "ws":
         need = L.clipmi_adapter_bwd_ws(R, D, A)
-        nwg = R  # adp_rb(4) = 1 row per workgroup
-        assert need == (R * (D + A) + nwg * (3 * D + A)) * 4
+        assert need >= (R * (D + A)) * 4  # dz + d_pre (fp32-sized) + the LN / column-sum scratch
         st = L.clipmi_adapter_bwd(None, 0, R, D, A, p, D, p, D, p, p, p, p, p, p, p, p, 1, p, D, *([None] * 6), p,
                                   need - 4)
     else:

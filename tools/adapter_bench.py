@@ -1,6 +1,8 @@
-"""Pooled-row adapter forward + backward (GPU): the fused clipmi_adapter_fwd / _bwd against the
-GEMM path AdapterFn takes on full hidden states, at the bench configs' per-GPU rows.
-  python tools/adapter_bench.py [R ...]     (default 1024; D 512 / 768 / 1024, A 256, bf16)"""
+"""Pooled-row adapter forward + backward (GPU): the one-call C-ABI entry points clipmi_adapter_fwd /
+clipmi_adapter_bwd (towers.AdapterFn since round 5) against the same kernels issued one by one from
+Python (the round-4 AdapterFn GEMM path: two GEMMs + LayerNorm forward, LN' + four GEMMs backward).
+Both must match bitwise; the times show what the single call saves in launch overhead.
+  python tools/adapter_bench.py [R ...]     (default 256 1024 4096; D 512 / 768 / 1024, A 256, bf16)"""
 import os
 import sys
 import types
@@ -8,7 +10,7 @@ import types
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vlm-clip_amd"))
 import torch  # noqa: E402
 
-from clipmi import synth, towers as T  # noqa: E402
+from clipmi import _lib, kernels as K, synth, towers as T  # noqa: E402
 from clipmi.modules import AdapterParams  # noqa: E402
 
 
@@ -25,7 +27,46 @@ def timed(f, n=50):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-for R in [int(a) for a in sys.argv[1:]] or [1024]:
+def python_sequence(mod, x2, dy2):
+    """The library kernels one call at a time (forward, then backward into fresh fp32 grads)."""
+    arena, dtype = mod.arena, torch.bfloat16
+    Dh, A = mod.hidden, mod.bottleneck
+    R = x2.shape[0]
+    s, dc = K.stream(), T.dcode(dtype)
+    wbuf = T._wbuf(arena, dtype)
+    dn, up = mod.names
+    pre = torch.empty(R, A, dtype=dtype, device="cuda")
+    act = torch.empty(R, A, dtype=dtype, device="cuda")
+    K.gemm(R, A, Dh, x2, Dh, True, arena.view(f"{dn}.weight", wbuf), Dh, True, act, A,
+           bias=arena.view(f"{dn}.bias", wbuf), aux=pre, ldaux=A, flags=_lib.EPI_BIAS | _lib.EPI_GELU | _lib.EPI_STORE_PRE)
+    z = torch.empty(R, Dh, dtype=dtype, device="cuda")
+    K.gemm(R, Dh, A, act, A, True, arena.view(f"{up}.weight", wbuf), A, True, z, Dh,
+           bias=arena.view(f"{up}.bias", wbuf), residual=x2, ldr=Dh, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
+    y = torch.empty(R, Dh, dtype=dtype, device="cuda")
+    st = torch.empty(2, R, device="cuda")
+    T.call("clipmi_layernorm_fwd", s, dc, T.P_(z), Dh, T.P_(y), Dh, arena.ptr("layer_norm.weight", wbuf),
+           arena.ptr("layer_norm.bias", wbuf), T.P_(st[0]), T.P_(st[1]), R, Dh, 1e-5, None, None, 0)
+    g = {k: torch.zeros_like(v, dtype=torch.float32) for k, v in
+         (("dw", arena.view(f"{dn}.weight", wbuf)), ("db", arena.view(f"{dn}.bias", wbuf)),
+          ("uw", arena.view(f"{up}.weight", wbuf)), ("ub", arena.view(f"{up}.bias", wbuf)),
+          ("lw", arena.view("layer_norm.weight", wbuf)), ("lb", arena.view("layer_norm.bias", wbuf)))}
+    dz = torch.empty(R, Dh, dtype=dtype, device="cuda")
+    lws = T._ws(_lib.lib().clipmi_layernorm_bwd_ws(R, Dh), "cuda")
+    T.call("clipmi_layernorm_bwd", s, dc, T.P_(dy2), Dh, T.P_(z), Dh, T.P_(st[0]), T.P_(st[1]),
+           arena.ptr("layer_norm.weight", wbuf), T.P_(dz), Dh, None, 0, T.P_(g["lw"]), T.P_(g["lb"]), 1, T.P_(lws),
+           lws.numel(), R, Dh)
+    K.gemm(Dh, A, R, dz, Dh, False, act, A, False, g["uw"], A, flags=_lib.EPI_BETA, bias_grad=g["ub"])
+    dpre = torch.empty(R, A, dtype=dtype, device="cuda")
+    K.gemm(R, A, Dh, dz, Dh, True, arena.view(f"{up}.weight", wbuf), A, False, dpre, A, aux=pre, ldaux=A,
+           flags=_lib.EPI_DGELU)
+    K.gemm(A, Dh, R, dpre, A, False, x2, Dh, False, g["dw"], Dh, flags=_lib.EPI_BETA, bias_grad=g["db"])
+    dx = torch.empty(R, Dh, dtype=dtype, device="cuda")
+    K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
+           flags=_lib.EPI_RESID)
+    return y, dx, g
+
+
+for R in [int(a) for a in sys.argv[1:]] or [256, 1024, 4096]:
     for D in (512, 768, 1024):
         mod = AdapterParams(D, 256, "cuda", ln=True, shadow=True)
         mod.load_numpy(synth.adapter_state_dict(D, 256, 7, "text_adapter"))
@@ -33,13 +74,21 @@ for R in [int(a) for a in sys.argv[1:]] or [1024]:
         anchor = next(iter(mod.parameters()))
         x = torch.randn(R, 1, D, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
         gy = torch.randn(R, 1, D, device="cuda", dtype=torch.bfloat16)
-        res = {}
-        for name, cap in (("fused", 4096), ("gemm", 0)):
-            T.AdapterFn.FUSED_MAX_ROWS = cap
-            fwd = lambda: T.AdapterFn.apply(x.detach(), anchor, rt, mod, False)
-            def fb():
-                y = T.AdapterFn.apply(x, anchor, rt, mod, True)
-                y.backward(gy)
-            res[name] = (timed(fwd), timed(fb))
-        print(f"R={R} D={D} A=256: fused fwd {res['fused'][0]:6.1f} us fwd+bwd {res['fused'][1]:6.1f} us | "
-              f"gemm path fwd {res['gemm'][0]:6.1f} us fwd+bwd {res['gemm'][1]:6.1f} us", flush=True)
+        fwd = lambda: T.AdapterFn.apply(x.detach(), anchor, rt, mod, False)
+
+        def fb():
+            y = T.AdapterFn.apply(x, anchor, rt, mod, True)
+            y.backward(gy)
+        t_call = (timed(fwd), timed(fb))
+        x2, dy2 = x.detach().reshape(R, D), gy.reshape(R, D)
+        t_seq = timed(lambda: python_sequence(mod, x2, dy2))
+        # bitwise: the one-call path equals the kernel sequence
+        for p in mod.parameters():
+            p.grad = None
+        x.grad = None
+        y1 = T.AdapterFn.apply(x, anchor, rt, mod, True)
+        y1.backward(gy)
+        y2, dx2, g2 = python_sequence(mod, x2, dy2)
+        same = torch.equal(y1.reshape(R, D), y2) and torch.equal(x.grad.reshape(R, D), dx2)
+        print(f"R={R} D={D} A=256: C-ABI call fwd {t_call[0]:6.1f} us fwd+bwd {t_call[1]:6.1f} us | "
+              f"python kernel sequence fwd+bwd {t_seq:6.1f} us | outputs bitwise equal: {same}", flush=True)

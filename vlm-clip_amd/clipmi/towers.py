@@ -518,21 +518,10 @@ class TextTowerFn(torch.autograd.Function):
 class AdapterFn(torch.autograd.Function):
     """y = LN(up(gelu(down(x))) + x)  (ln=False: up(gelu(down(x))) + x).
 
-    Two GEMMs with fused epilogues (down + bias + gelu_erf with the pre-activation saved; up + bias
-    + residual) and the LayerNorm kernel; backward LN' + four GEMMs.  With R <= FUSED_MAX_ROWS the
-    one-launch clipmi_adapter_fwd / two-launch clipmi_adapter_bwd run instead (same saved tensors).
-    They are correct (tests/test_gpu_kernels.py) but measured slower than the GEMM path at every
-    bench size -- R = 256: forward 51 vs 32 us, backward 361 vs 150 us of GPU time; R = 4096: the
-    backward's serial weight-gradient loop is 10x the MFMA GEMMs (profiles/r04_adapter_fused_vs_gemm.log)
-    -- so the product path keeps the GEMMs (FUSED_MAX_ROWS = 0) and the entry points serve FFI
-    callers that want the adapter as one call."""
-
-    FUSED_MAX_ROWS = 0
-
-    @staticmethod
-    def _fused(mod, R):
-        Dh, A = mod.hidden, mod.bottleneck
-        return 0 < R <= AdapterFn.FUSED_MAX_ROWS and Dh % 8 == 0 and A % 8 == 0 and 32 * (2 * Dh + A) <= 160 * 1024
+    One C-ABI call per direction (csrc/adapter.cpp): clipmi_adapter_fwd runs the down GEMM (+ bias +
+    gelu_erf, pre-activation saved), the up GEMM (+ bias + residual) and the LayerNorm kernel;
+    clipmi_adapter_bwd runs LN' and the four GEMMs (fused bias gradients in bf16).  The same entry
+    points are the FFI binding of INTEGRATION.md, so the Python mirror and an FFI caller run one path."""
 
     @staticmethod
     def forward(ctx, x, anchor, runtime, mod, need):
@@ -546,37 +535,20 @@ class AdapterFn(torch.autograd.Function):
         dc = dcode(dtype)
         wbuf = _wbuf(arena, dtype)
         dn, up = mod.names
-        fused = AdapterFn._fused(mod, R)
         pre = torch.empty(R, A, dtype=dtype, device=dev) if need else None
-        if fused:
-            y = torch.empty(R, Dh, dtype=dtype, device=dev)
-            act = torch.empty(R, A, dtype=dtype, device=dev) if need else None
-            z = torch.empty(R, Dh, dtype=dtype, device=dev) if need and mod.has_ln else None
-            stats = torch.empty(2, R, dtype=torch.float32, device=dev) if need and mod.has_ln else None
-            ln_ptr = (lambda n: arena.ptr(n, wbuf)) if mod.has_ln else (lambda n: None)
-            call("clipmi_adapter_fwd", s, dc, R, Dh, A, P_(x2), Dh, arena.ptr(f"{dn}.weight", wbuf),
-                 arena.ptr(f"{dn}.bias", wbuf), arena.ptr(f"{up}.weight", wbuf), arena.ptr(f"{up}.bias", wbuf),
-                 ln_ptr("layer_norm.weight"), ln_ptr("layer_norm.bias"), 1e-5, int(mod.has_ln), P_(y), Dh, P_(pre),
-                 P_(act), P_(z), P_(stats[0]) if stats is not None else None,
-                 P_(stats[1]) if stats is not None else None)
-        else:
-            act = torch.empty(R, A, dtype=dtype, device=dev)
-            flags = _lib.EPI_BIAS | _lib.EPI_GELU | (_lib.EPI_STORE_PRE if need else 0)
-            K.gemm(R, A, Dh, x2, Dh, True, arena.view(f"{dn}.weight", wbuf), Dh, True, act, A,
-                   bias=arena.view(f"{dn}.bias", wbuf), aux=pre, ldaux=A, flags=flags)
-            z = torch.empty(R, Dh, dtype=dtype, device=dev)
-            K.gemm(R, Dh, A, act, A, True, arena.view(f"{up}.weight", wbuf), A, True, z, Dh,
-                   bias=arena.view(f"{up}.bias", wbuf), residual=x2, ldr=Dh, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
-            if mod.has_ln:
-                y = torch.empty(R, Dh, dtype=dtype, device=dev)
-                stats = torch.empty(2, R, dtype=torch.float32, device=dev)
-                call("clipmi_layernorm_fwd", s, dc, P_(z), Dh, P_(y), Dh, arena.ptr("layer_norm.weight", wbuf),
-                     arena.ptr("layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, Dh, 1e-5, None, None, 0)
-            else:
-                y, stats = z, None
+        act = torch.empty(R, A, dtype=dtype, device=dev)
+        y = torch.empty(R, Dh, dtype=dtype, device=dev)
+        z = torch.empty(R, Dh, dtype=dtype, device=dev) if mod.has_ln else None
+        stats = torch.empty(2, R, dtype=torch.float32, device=dev) if mod.has_ln else None
+        ln_ptr = (lambda n: arena.ptr(n, wbuf)) if mod.has_ln else (lambda n: None)
+        call("clipmi_adapter_fwd", s, dc, R, Dh, A, P_(x2), Dh, arena.ptr(f"{dn}.weight", wbuf),
+             arena.ptr(f"{dn}.bias", wbuf), arena.ptr(f"{up}.weight", wbuf), arena.ptr(f"{up}.bias", wbuf),
+             ln_ptr("layer_norm.weight"), ln_ptr("layer_norm.bias"), 1e-5, int(mod.has_ln), P_(y), Dh, P_(pre),
+             P_(act), P_(z), P_(stats[0]) if stats is not None else None,
+             P_(stats[1]) if stats is not None else None)
         if need:
             ctx.save = (x2, pre, act, z, stats)
-            ctx.mod, ctx.rt, ctx.shape, ctx.fused = mod, runtime, shp, fused
+            ctx.mod, ctx.rt, ctx.shape = mod, runtime, shp
         return y.view(shp)
 
     @staticmethod
@@ -597,44 +569,15 @@ class AdapterFn(torch.autograd.Function):
         dn, up = mod.names
         dy2 = dy.to(dtype).reshape(R, Dh).contiguous()
         dx = torch.empty(R, Dh, dtype=dtype, device=dev)
-        if ctx.fused:
-            gp = (lambda n: arena.ptr(n, g)) if train_params else (lambda n: None)
-            lnp = gp if mod.has_ln else (lambda n: None)
-            ws = _ws(_lib.lib().clipmi_adapter_bwd_ws(R, Dh, A), dev)
-            call("clipmi_adapter_bwd", s, dc, R, Dh, A, P_(dy2), Dh, P_(x2), Dh, P_(pre), P_(act), P_(z),
-                 P_(stats[0]) if stats is not None else None, P_(stats[1]) if stats is not None else None,
-                 arena.ptr(f"{dn}.weight", wbuf), arena.ptr(f"{up}.weight", wbuf),
-                 arena.ptr("layer_norm.weight", wbuf) if mod.has_ln else None, int(mod.has_ln), P_(dx), Dh,
-                 gp(f"{dn}.weight"), gp(f"{dn}.bias"), gp(f"{up}.weight"), gp(f"{up}.bias"),
-                 lnp("layer_norm.weight"), lnp("layer_norm.bias"), P_(ws), ws.numel())
-            ctx.save = None
-            return dx.view(ctx.shape), None, None, None, None
-        if mod.has_ln:
-            dz = torch.empty(R, Dh, dtype=dtype, device=dev)
-            lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, Dh), dev)
-            call("clipmi_layernorm_bwd", s, dc, P_(dy2), Dh, P_(z), Dh, P_(stats[0]), P_(stats[1]),
-                 arena.ptr("layer_norm.weight", wbuf), P_(dz), Dh, None, 0,
-                 arena.ptr("layer_norm.weight", g) if train_params else None,
-                 arena.ptr("layer_norm.bias", g) if train_params else None, 1, P_(lws), lws.numel(), R, Dh)
-        else:
-            dz = dy2
-        cws = _ws(_lib.lib().clipmi_colsum_ws(R, max(Dh, A)), dev)
-        bf = dtype == torch.bfloat16
-        if train_params:
-            K.gemm(Dh, A, R, dz, Dh, False, act, A, False, arena.view(f"{up}.weight", g), A, flags=_lib.EPI_BETA,
-                   bias_grad=arena.view(f"{up}.bias", g) if bf else None)
-            if not bf:
-                call("clipmi_colsum", s, dc, P_(dz), Dh, R, Dh, arena.ptr(f"{up}.bias", g), 1, P_(cws), cws.numel())
-        dpre = torch.empty(R, A, dtype=dtype, device=dev)
-        K.gemm(R, A, Dh, dz, Dh, True, arena.view(f"{up}.weight", wbuf), A, False, dpre, A, aux=pre, ldaux=A,
-               flags=_lib.EPI_DGELU)
-        if train_params:
-            K.gemm(A, Dh, R, dpre, A, False, x2, Dh, False, arena.view(f"{dn}.weight", g), Dh, flags=_lib.EPI_BETA,
-                   bias_grad=arena.view(f"{dn}.bias", g) if bf else None)
-            if not bf:
-                call("clipmi_colsum", s, dc, P_(dpre), A, R, A, arena.ptr(f"{dn}.bias", g), 1, P_(cws), cws.numel())
-        K.gemm(R, Dh, A, dpre, A, True, arena.view(f"{dn}.weight", wbuf), Dh, False, dx, Dh, residual=dz, ldr=Dh,
-               flags=_lib.EPI_RESID)
+        gp = (lambda n: arena.ptr(n, g)) if train_params else (lambda n: None)
+        lnp = gp if mod.has_ln else (lambda n: None)
+        ws = _ws(_lib.lib().clipmi_adapter_bwd_ws(R, Dh, A), dev)
+        call("clipmi_adapter_bwd", s, dc, R, Dh, A, P_(dy2), Dh, P_(x2), Dh, P_(pre), P_(act), P_(z),
+             P_(stats[0]) if stats is not None else None, P_(stats[1]) if stats is not None else None,
+             arena.ptr(f"{dn}.weight", wbuf), arena.ptr(f"{up}.weight", wbuf),
+             arena.ptr("layer_norm.weight", wbuf) if mod.has_ln else None, int(mod.has_ln), P_(dx), Dh,
+             gp(f"{dn}.weight"), gp(f"{dn}.bias"), gp(f"{up}.weight"), gp(f"{up}.bias"),
+             lnp("layer_norm.weight"), lnp("layer_norm.bias"), P_(ws), ws.numel())
         ctx.save = None  # released with backward (see VisionTowerFn)
         return dx.view(ctx.shape), None, None, None, None
 
