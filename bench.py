@@ -61,7 +61,8 @@ def parse():
                          "fp32: the parity mode (f32 operands end to end), priced against the f32 MFMA peak")
     ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES) + list(FAMILIES_FP32),
                     help="family reported as `roofline` (default: the one with the most measured time)")
-    ap.add_argument("--cpu-sample", type=int, default=8, help="pairs per CPU-baseline step (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=32,
+                    help="pairs per CPU-baseline step (SURVEY 8d: B = 32; 0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--launch-check", action="store_true",
                     help="test hook: each rank prints its rank/world and exits before touching the GPU")
@@ -142,6 +143,18 @@ def algorithmic_bytes(cfg, B, train):
     return {k: round(v) for k, v in out.items()}
 
 
+def _cpu_model():
+    """The host CPU's model string (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_adapter(cfg, B, steps, threads):
     """Oracle adapter fine-tune step (frozen towers, configs 2/4/5) on the host: the towers' forward,
     the adapters on the pooled rows (model_m.py:77-125), the contrastive loss and its backward into
@@ -169,7 +182,7 @@ def cpu_baseline_adapter(cfg, B, steps, threads):
         log(f"cpu baseline step {it}: {time.perf_counter() - t0:.2f} s")
     times.sort()
     med = times[len(times) // 2]
-    return {"value": round(B / med, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": round(B / med, 3), "unit": "pairs/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
             "sample": f"oracle/clip_ref.py {cfg.name} adapter fine-tune step (frozen towers fwd + adapters fwd/bwd + "
                       f"InfoNCE) fp32, B={B}, median of {steps} steps after 1 warm-up, torch CPU threads={threads}"}
 
@@ -215,7 +228,7 @@ def cpu_baseline(cfg, B, steps, adapters=False):
         log(f"cpu baseline step {it}: {time.perf_counter() - t0:.2f} s")
     times.sort()
     med = times[len(times) // 2]
-    return {"value": round(B / med, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": round(B / med, 3), "unit": "pairs/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
             "sample": f"oracle/clip_ref.py {cfg.name} full fine-tune step (fwd+bwd+AdamW) fp32, B={B}, "
                       f"median of {steps} steps after 1 warm-up, torch CPU threads={threads}"}
 

@@ -71,8 +71,8 @@ typedef struct clipmi_gemm_desc {
    * bytes, both k-major, K % 128 == 0; a_scale / b_scale are E8M0 bytes [rows][K/32] (OCP MX:
    * element value = fp8 * 2^(scale - 127)); v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation,
    * the bf16 epilogues.  c_dtype == CLIPMI_FP8 (flags bias and/or quick_gelu / gelu only, ldc == N,
-   * N % 32 == 0): C is written as MXFP8 too, e4m3 bytes [M, N] and E8M0 scales c_scale [M, N/32]
-   * (fc1 -> fc2 without a bf16 round trip). */
+   * N % 32 == 0, C 16-byte and c_scale 2-byte aligned): C is written as MXFP8 too, e4m3 bytes [M, N]
+   * and E8M0 scales c_scale [M, N/32] (fc1 -> fc2 without a bf16 round trip). */
   const uint8_t* a_scale;
   const uint8_t* b_scale;
   uint8_t* c_scale;
@@ -94,6 +94,12 @@ typedef struct clipmi_gemm_desc {
 #define CLIPMI_EPI_MUL_AUX 512
 
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
+/* Strided batch of nb1 x nb2 fp32 products (exact f32; flags: beta only): product z = i1 * nb2 + i2 reads
+ * A + i1 * sa1 + i2 * sa2, B + i1 * sb1 + i2 * sb2 and writes C + i1 * sc1 + i2 * sc2 (elements), the
+ * rest as clipmi_gemm.  One launch for the per-(sample, head) score / context products of attention at
+ * head widths the flash kernels do not take (peclip ContextAdapter / SharedAdapter, adapter/peclip.py:21-48). */
+int clipmi_gemm_batched(void* stream, const clipmi_gemm_desc* d, int nb1, int nb2, int64_t sa1, int64_t sa2,
+                        int64_t sb1, int64_t sb2, int64_t sc1, int64_t sc2);
 /* Diagnostic (no reference counterpart): arm / disarm (nullptr) the in-kernel s_memtime stamps of
  * the 4-wave GEMM's timing variant (force_small_tile = 22); buf holds 512 * 4 * 128 u64 of device
  * memory (layout: csrc/gemm4.hip, reader: tools/w4_stamps.py). */
@@ -107,7 +113,8 @@ int clipmi_quant_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, int6
 /* ---- LayerNorm ([HF] modeling_clip.py:357,359,605,642,559; adapter/clip_adapter.py:15,142) -------
  * y = LN(x [+ pos[row % period] (+ cls at row % period == 0)]) * w + b; mean/rstd saved (fp32).
  * With pos != NULL the sum is written back to x: the vision embedding ([HF] :209-219) fused
- * into pre_layrnorm. Weights in the activation dtype. D % 64 == 0, D <= 1024. */
+ * into pre_layrnorm. Weights in the activation dtype. 1 <= D <= 4096: register-resident kernels for D / 64
+ * in {1, 2, 3, 4, 6, 8, 12, 16} (every CLIP width), a one-wave-per-row kernel for any other width. */
 int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy, const void* w,
                          const void* b, float* mean, float* rstd, int R, int D, float eps, const void* pos,
                          const void* cls, int period);
@@ -117,7 +124,7 @@ int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y,
 int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, uint8_t* q8, uint8_t* s8,
                                const void* w, const void* b, float* mean, float* rstd, int R, int D, float eps);
 int64_t clipmi_layernorm_bwd_ws(int R, int D);
-/* dx = [dres +] LN'(dy); dw/db (fp32, may be NULL) accumulate when beta_wb. */
+/* dx = [dres +] LN'(dy); dw/db (fp32, may be NULL) accumulate when beta_wb.  Widths as clipmi_layernorm_fwd. */
 int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                          const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                          int64_t ldres, float* dw, float* db, int beta_wb, void* ws, int64_t ws_bytes, int R, int D);
@@ -137,7 +144,7 @@ int clipmi_period_sum(void* stream, int dtype, const void* x, int64_t ldx, int n
  * down GEMM (+ bias + gelu_erf; pre-activation stored when pre != NULL), up GEMM (+ bias + residual),
  * LayerNorm -- the path the Python mirror runs.  act [R, A] is required (it carries the bottleneck
  * between the GEMMs); with ln also z [R, D] (the pre-LN sum) and mean / rstd [R] (fp32).  pre [R, A]
- * is saved for the backward (NULL in inference).  D % 8 == 0, A % 8 == 0; with ln D % 64 == 0, D <= 1024. */
+ * is saved for the backward (NULL in inference).  D % 8 == 0, A % 8 == 0; with ln D <= 4096. */
 int clipmi_adapter_fwd(void* stream, int dtype, int R, int D, int A, const void* x, int64_t ldx, const void* w_down,
                        const void* b_down, const void* w_up, const void* b_up, const void* ln_w, const void* ln_b,
                        float eps, int ln, void* y, int64_t ldy, void* pre, void* act, void* z, float* mean,
@@ -192,7 +199,7 @@ int clipmi_scatter_rows(void* stream, int dtype, const void* src, const int* idx
  * attention_mask: int64 [B, N] key padding (1 keep) or NULL; causal for the text tower. */
 int clipmi_attention_fwd(void* stream, int dtype, const void* qkv, void* o, float* lse, const int64_t* attention_mask,
                          int causal, int B, int H, int N, int D);
-/* The K/V-streaming forward with O written as MXFP8 (OCP e4m3 o8 [B*N, D] + E8M0 s8 [B*N, D/32],
+/* The K/V-streaming forward with O written as MXFP8 (OCP e4m3 o8 [B*N, D], 4-byte aligned + E8M0 s8 [B*N, D/32],
  * clipmi_quant_mxfp8's rule applied to the fp32 O): the fp8 towers' out-projection operand without a
  * bf16 round trip (BASELINE config 5).  bf16 q/k/v. */
 int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t* o8, uint8_t* s8, float* lse,
@@ -207,7 +214,9 @@ typedef struct clipmi_layer_w { /* activation dtype; qkv_w = [q;k;v] rows, [3D, 
 typedef struct clipmi_layer_grad { /* fp32, accumulated */
   float *ln1_w, *ln1_b, *qkv_w, *qkv_b, *out_w, *out_b, *ln2_w, *ln2_b, *fc1_w, *fc1_b, *fc2_w, *fc2_b;
 } clipmi_layer_grad;
-typedef struct clipmi_layer_act { /* saved activations; pre == NULL in inference */
+typedef struct clipmi_layer_act { /* saved activations; pre == NULL in inference.  The fp8 encoder
+  * (dtype CLIPMI_FP8) with N > 288 sends the attention output straight to the out-projection's
+  * MXFP8 operand and does NOT write o: read act[l].o only after a bf16 / f32 forward or N <= 288. */
   void *x_in, *ln1, *qkv, *o, *h, *ln2, *pre, *act;
   float *mean1, *rstd1, *lse, *mean2, *rstd2;
 } clipmi_layer_act;

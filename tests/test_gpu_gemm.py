@@ -294,7 +294,7 @@ def test_gemm_4wave_matches_pingpong(var, bkm, flags, M, N, K):
                                               (20000, 2304, 768, 4), (300, 768, 768, 3), (4100, 520, 264, 2),
                                               (9000, 768, 768, 1)])
 @pytest.mark.parametrize("bias", [False, True])
-@pytest.mark.parametrize("var", [28, 32])
+@pytest.mark.parametrize("var", [28])
 def test_wgrad_4wave_matches_8wave(T, Nout, Kin, split, bias, var):
     """Weight gradient on the persistent 4-wave kernel (gemm4.hip, variant 28) vs the 8-wave wgrad
     kernel (variant 4): the same k order of MFMA accumulation per output element, so bitwise-equal

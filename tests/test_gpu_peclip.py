@@ -90,3 +90,72 @@ def test_textual_adapter_module_matches_reference(golden, precision):
     assert _rel(x.grad.cpu().numpy(), g["textual_gx"]) < tol
     for k, p in mod.named_parameters():
         assert _rel(p.grad.cpu().numpy(), g[f"textual_g/{k}"]) < (tol if precision == "fp32" else 0.1), k
+
+
+def _prof_count(labels, fn):
+    """Launches of the given GEMM variant labels while fn() runs (the library's live profiler)."""
+    import ctypes
+    from clipmi import _lib
+    L = _lib.lib()
+    L.clipmi_prof_arm.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.clipmi_prof_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
+    cap = 4096
+    _lib.check(L.clipmi_prof_arm(",".join(labels).encode(), cap), "prof_arm")
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        L.clipmi_prof_disarm()
+    ms, fl = (ctypes.c_float * cap)(), (ctypes.c_double * cap)()
+    return L.clipmi_prof_read(cap, ms, fl)
+
+
+@pytest.mark.parametrize("D,heads,B,N", [(192, 4, 5, 33), (128, 4, 3, 50), (320, 4, 2, 17), (96, 2, 3, 11)])
+def test_general_head_width_batched_matches_torch(D, heads, B, N):
+    """head_dim 48 / 32 / 80 / 48 (ContextAdapter with num_heads that do not give 64; D = 320 and 96 take
+    the any-width LayerNorm kernels, D = 96 is the reference's own init-test width): the strided-batched
+    fp32 path (clipmi_gemm_batched + row softmax over all B * H * N rows) vs PyTorch's own
+    nn.MultiheadAttention + nn.LayerNorm in fp32 with the same parameters (output, input gradient,
+    every parameter gradient: max |diff| / max |ref| < 2e-4), and its GEMM launch count does not grow
+    with B * H: the same number of launches at batch B and batch 1."""
+    from clipmi import peclip
+    torch.manual_seed(0)
+    mod = peclip.ContextAdapter(D, heads, device="cuda", precision="fp32")
+    assert mod.attention_precision == "fp32" and mod.head_dim != 64
+    ref_attn = torch.nn.MultiheadAttention(D, heads, batch_first=True).cuda()
+    ref_ln = torch.nn.LayerNorm(D).cuda()
+    sd = mod.state_dict()
+    with torch.no_grad():
+        ref_attn.in_proj_weight.copy_(sd["mhsa.in_proj_weight"])
+        ref_attn.in_proj_bias.copy_(sd["mhsa.in_proj_bias"])
+        ref_attn.out_proj.weight.copy_(sd["mhsa.out_proj.weight"])
+        ref_attn.out_proj.bias.copy_(sd["mhsa.out_proj.bias"])
+        ref_ln.weight.copy_(torch.linspace(0.5, 1.5, D))
+        ref_ln.bias.copy_(torch.linspace(-0.1, 0.1, D))
+        sd["layer_norm.weight"], sd["layer_norm.bias"] = ref_ln.weight.detach().cpu(), ref_ln.bias.detach().cpu()
+    mod.load_state_dict({k: v.cpu() for k, v in sd.items()})
+    x = torch.randn(B, N, D, device="cuda")
+    gy = torch.randn(B, N, D, device="cuda")
+    xa, xr = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya = mod(xa)
+    ya.backward(gy)
+    yr = ref_ln(ref_attn(xr, xr, xr, need_weights=False)[0] + xr)
+    yr.backward(gy)
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        return float((a - b).abs().max() / b.abs().max().clamp_min(1e-6))
+    assert rel(ya, yr) < 2e-4 and rel(xa.grad, xr.grad) < 2e-4
+    pairs = {"mhsa.in_proj_weight": ref_attn.in_proj_weight, "mhsa.in_proj_bias": ref_attn.in_proj_bias,
+             "mhsa.out_proj.weight": ref_attn.out_proj.weight, "mhsa.out_proj.bias": ref_attn.out_proj.bias,
+             "layer_norm.weight": ref_ln.weight, "layer_norm.bias": ref_ln.bias}
+    got = dict(mod.named_parameters())
+    for k, rp in pairs.items():
+        assert rel(got[k].grad, rp.grad) < 2e-4, k
+
+    def step(bb):
+        xx = torch.randn(bb, N, D, device="cuda", requires_grad=True)
+        mod(xx).backward(torch.randn(bb, N, D, device="cuda"))
+    labels = ["gemm_f32_batched", "gemm_f32"]
+    assert _prof_count(labels, lambda: step(B)) == _prof_count(labels, lambda: step(1))
+    assert _prof_count(["gemm_f32_batched"], lambda: step(B)) == 6  # scores, context; dP, dQ, dK, dV

@@ -53,6 +53,8 @@ _declare("clipmi_version", ctypes.c_int, [])
 _declare("clipmi_build_digest", ctypes.c_char_p, [])
 _declare("clipmi_last_error", ctypes.c_char_p, [])
 _declare("clipmi_gemm", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc)])
+_declare("clipmi_gemm_batched", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc), ctypes.c_int, ctypes.c_int]
+         + [ctypes.c_int64] * 6)
 
 
 def declare(name, argtypes, restype=ctypes.c_int):

@@ -62,6 +62,26 @@ def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, resi
     return C
 
 
+def gemm_batched(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, nb1, nb2, sa, sb, sc, *, alpha=1.0,
+                 beta=False):
+    """nb1 x nb2 fp32 products in one launch: product (i1, i2) reads A + i1 sa[0] + i2 sa[1], B + ...,
+    writes C + i1 sc[0] + i2 sc[1] (element strides); see include/clipmi.h clipmi_gemm_batched."""
+    _on_gpu(A, B, C)
+    if not (A.dtype == B.dtype == C.dtype == torch.float32):
+        raise ValueError("gemm_batched: fp32 operands and output")
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = A.data_ptr(), lda, int(a_kmajor)
+    d.B, d.ldb, d.b_kmajor = B.data_ptr(), ldb, int(b_kmajor)
+    d.C, d.ldc = C.data_ptr(), ldc
+    d.alpha, d.flags = alpha, (_lib.EPI_BETA if beta else 0)
+    d.ab_dtype = d.c_dtype = d.bias_dtype = F32
+    d.split_k = 1
+    _lib.check(_lib.lib().clipmi_gemm_batched(stream(), ctypes.byref(d), nb1, nb2, sa[0], sa[1], sb[0], sb[1],
+                                               sc[0], sc[1]), "clipmi_gemm_batched")
+    return C
+
+
 def linear(x, w, bias=None, *, act=None, residual=None, out=None, pre_out=None):
     """y = act(x @ w.T + bias) (+ residual): nn.Linear forward on the MFMA GEMM."""
     x2 = x.reshape(-1, x.shape[-1])

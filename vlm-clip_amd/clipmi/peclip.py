@@ -9,12 +9,16 @@ arguments and state-dict keys (checkpoints load either way).
 GEMM [B*N, 3D] (q | k | v, head h at h*head_dim -- the layout clipmi_attention reads), softmax
 attention with scale head_dim^-0.5 and no mask, the out-projection GEMM with its bias and the
 residual x fused into the epilogue, then the LayerNorm kernel (eps 1e-5).  head_dim 64 and
-N <= 4096 run the flash attention kernels (clipmi_attention_fwd/bwd); other head widths take a
-per-(sample, head) path of fp32 GEMMs and row-softmax kernels.  Every op is a libclipmi GPU kernel;
-there is no CPU path (construction works anywhere, forward needs CUDA tensors).
+N <= 4096 run the flash attention kernels (clipmi_attention_fwd/bwd); other head widths run the
+scores, softmax and context of every (sample, head) as strided-batched exact-fp32 GEMMs
+(clipmi_gemm_batched) and row-softmax kernels over all rows: three launches forward, five backward,
+whatever B * H is.  Every op is a libclipmi GPU kernel; there is no CPU path (construction works
+anywhere, forward needs CUDA tensors).
 
 ``precision`` is the compute precision, as in CLIPWithAdapters: "fp32" (parity) or "bf16" (MFMA
-operands from the bf16 shadow of the fp32 master weights, fp32 accumulation and gradients).
+operands from the bf16 shadow of the fp32 master weights, fp32 accumulation and gradients).  The
+general-head-width path above computes in fp32 under either setting (``attention_precision`` says
+which one a module runs: "bf16" only with head_dim 64).
 Initialisation draws from torch's default generator in nn.Linear / nn.MultiheadAttention's order,
 so under the same torch.manual_seed the parameters equal the reference module's.
 """
@@ -99,6 +103,9 @@ class _MHSAResidualLN(ArenaModule):
         super().__init__(_mhsa_specs(input_dim), device, shadow=dtype == torch.bfloat16)
         self.embed_dim, self.num_heads, self.head_dim = input_dim, num_heads, input_dim // num_heads
         self.dtype = dtype
+        # the compute precision of the whole block: the head_dim-64 flash path follows ``precision``,
+        # other head widths run exact fp32 (module docstring)
+        self.attention_precision = ("bf16" if dtype == torch.bfloat16 else "fp32") if self.head_dim == 64 else "fp32"
         D = input_dim
         with torch.no_grad():
             # nn.MultiheadAttention.__init__: out_proj (an nn.Linear: kaiming weight, uniform bias) is
@@ -118,8 +125,8 @@ class _MHSAResidualLN(ArenaModule):
                                  "query tensor")
         if x.shape[-1] != D:
             raise AssertionError(f"was expecting embedding dimension of {D}, but got {x.shape[-1]}")
-        if D % 64 or D > 1024:  # the LayerNorm kernel's row layout (clipmi_layernorm_fwd)
-            raise ValueError(f"clipmi ContextAdapter/SharedAdapter need input_dim % 64 == 0 and <= 1024 (got {D})")
+        if D > 4096:  # clipmi_layernorm_fwd's widest row
+            raise ValueError(f"clipmi ContextAdapter/SharedAdapter need input_dim <= 4096 (got {D})")
         anchor = next(self.parameters())
         need = torch.is_grad_enabled() and (x.requires_grad or self.arena.any_requires_grad())
         xb = x if x.dim() == 3 else x.unsqueeze(0)
@@ -165,16 +172,13 @@ class MHSAResidualLNFn(torch.autograd.Function):
         if fast:
             lse = torch.empty(B * H * N, dtype=torch.float32, device=dev)
             call("clipmi_attention_fwd", s, dc, P_(qkv), P_(o), P_(lse), None, 0, B, H, N, D)
-        else:
+        else:  # three launches for every (sample, head): scores, row softmax, context
             P = torch.empty(B, H, N, N, dtype=torch.float32, device=dev)
             scale = hd ** -0.5
-            for b in range(B):
-                r = slice(b * N, (b + 1) * N)
-                for h in range(H):
-                    c = h * hd
-                    K.gemm(N, N, hd, qkv[r, c:], 3 * D, True, qkv[r, D + c:], 3 * D, True, P[b, h], N)
-                    call("clipmi_softmax_rows", s, P_(P[b, h]), P_(P[b, h]), N, N, scale)
-                    K.gemm(N, hd, N, P[b, h], N, True, qkv[r, 2 * D + c:], 3 * D, False, o[r, c:], D)
+            sq, sp = (N * 3 * D, hd), (H * N * N, N * N)
+            K.gemm_batched(N, N, hd, qkv, 3 * D, True, qkv[:, D:], 3 * D, True, P, N, B, H, sq, sq, sp)
+            call("clipmi_softmax_rows", s, P_(P), P_(P), B * H * N, N, scale)
+            K.gemm_batched(N, hd, N, P, N, True, qkv[:, 2 * D:], 3 * D, False, o, D, B, H, sp, sq, (N * D, hd))
         K.gemm(R, D, D, o, D, True, W("mhsa.out_proj.weight"), D, True, z, D, bias=W("mhsa.out_proj.bias"),
                residual=x2, ldr=D, flags=_lib.EPI_BIAS | _lib.EPI_RESID)
         stats = torch.empty(2, R, dtype=torch.float32, device=dev)
@@ -230,18 +234,15 @@ class MHSAResidualLNFn(torch.autograd.Function):
         dqkv = e(R, 3 * D)
         if fast:
             call("clipmi_attention_bwd", s, dc, P_(qkv), P_(o), P_(lse), P_(do), P_(dqkv), None, 0, B, H, N, D)
-        else:
-            dS = torch.empty(N, N, dtype=torch.float32, device=dev)
+        else:  # five launches for every (sample, head)
+            dS = torch.empty(B, H, N, N, dtype=torch.float32, device=dev)
             scale = hd ** -0.5
-            for b in range(B):
-                r = slice(b * N, (b + 1) * N)
-                for h in range(H):
-                    c = h * hd
-                    K.gemm(N, N, hd, do[r, c:], D, True, qkv[r, 2 * D + c:], 3 * D, True, dS, N)
-                    call("clipmi_softmax_rows_bwd", s, P_(P[b, h]), P_(dS), P_(dS), N, N, scale)
-                    K.gemm(N, hd, N, dS, N, True, qkv[r, D + c:], 3 * D, False, dqkv[r, c:], 3 * D)
-                    K.gemm(N, hd, N, dS, N, False, qkv[r, c:], 3 * D, False, dqkv[r, D + c:], 3 * D)
-                    K.gemm(N, hd, N, P[b, h], N, False, do[r, c:], D, False, dqkv[r, 2 * D + c:], 3 * D)
+            sq, sp, so = (N * 3 * D, hd), (H * N * N, N * N), (N * D, hd)
+            K.gemm_batched(N, N, hd, do, D, True, qkv[:, 2 * D:], 3 * D, True, dS, N, B, H, so, sq, sp)  # dP
+            call("clipmi_softmax_rows_bwd", s, P_(P), P_(dS), P_(dS), B * H * N, N, scale)          # dS
+            K.gemm_batched(N, hd, N, dS, N, True, qkv[:, D:], 3 * D, False, dqkv, 3 * D, B, H, sp, sq, sq)  # dQ
+            K.gemm_batched(N, hd, N, dS, N, False, qkv, 3 * D, False, dqkv[:, D:], 3 * D, B, H, sp, sq, sq)  # dK
+            K.gemm_batched(N, hd, N, P, N, False, do, D, False, dqkv[:, 2 * D:], 3 * D, B, H, sp, so, sq)   # dV
         # in-projection: qkv = x Win^T + bin
         if train:
             K.gemm(3 * D, D, R, dqkv, 3 * D, False, x2, D, False, G("mhsa.in_proj_weight"), D, flags=_lib.EPI_BETA,

@@ -1791,9 +1791,13 @@ int bwd_pf_dispatch(const AttnP& p, int causal, hipStream_t s) {
   // two blocks per wave share and one block per wave does not
   const char* e = getenv("CLIPMI_ATTN_BWD_NW");
   const int nw = e ? atoi(e) : 8;
-  if (nw == 4 && !causal && p.N > 128 && p.N <= 224) {  // 4 waves x 4 blocks (NPAD <= 256 threads)
+#ifdef CLIPMI_GEMM_EXPERIMENTS  // 4 waves x 4 blocks (NPAD <= 256 threads): 1283 vs 880 us, experiments build only
+  if (nw == 4 && !causal && p.N > 128 && p.N <= 224) {
     launch_bwd_pf<false, 4, 4>(p, s);
-  } else if (p.N <= 128) {
+    return CLIPMI_OK;
+  }
+#endif
+  if (p.N <= 128) {
     if (causal) launch_bwd_pf<true, 4>(p, s); else launch_bwd_pf<false, 4>(p, s);
   } else if (nw == 16 && p.N <= 256) {
     if (causal) launch_bwd_pf<true, 16>(p, s); else launch_bwd_pf<false, 16>(p, s);
@@ -1846,6 +1850,7 @@ extern "C" int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
   CLIPMI_REQUIRE(N >= 1 && N <= ATTN_MAX_N_ANY, "N must be in [1, 4096]");
   CLIPMI_REQUIRE(qkv && o8 && s8 && lse, "operands");
+  CLIPMI_REQUIRE(((uintptr_t)o8 & 3) == 0, "o8 must be 4-byte aligned (the e4m3 rows go out as 32-bit stores)");
   if (B == 0) return CLIPMI_OK;
   AttnP p{(const bf16*)qkv, nullptr, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
   p.o8 = o8;

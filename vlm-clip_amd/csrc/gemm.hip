@@ -991,6 +991,12 @@ template <typename OutT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p, int akm, int bkm) {
   __shared__ float As[FK][FT + 4];
   __shared__ float Bs[FK][FT + 4];
+  if (p.nb2 > 0) {  // strided batch: this block's (i1, i2) slice of A, B, C
+    const int i1 = blockIdx.z / p.nb2, i2 = blockIdx.z - i1 * p.nb2;
+    p.A = (const float*)p.A + i1 * p.bsa1 + i2 * p.bsa2;
+    p.B = (const float*)p.B + i1 * p.bsb1 + i2 * p.bsb2;
+    p.C = (OutT*)p.C + i1 * p.bsc1 + i2 * p.bsc2;
+  }
   const float* A = (const float*)p.A;
   const float* B = (const float*)p.B;
   const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
@@ -1322,6 +1328,39 @@ extern "C" int clipmi_gemm_stamps(void* buf) {
   return CLIPMI_OK;
 }
 
+// Strided-batched fp32 GEMM (exact f32, SIMT kernel): nb1 x nb2 independent products C_z = alpha A_z B_z^T
+// (z = i1 * nb2 + i2, each operand offset by i1 * stride1 + i2 * stride2 elements), one launch.  The
+// per-(sample, head) products of peclip's general head width (adapter/peclip.py:21-48 through
+// nn.MultiheadAttention) without a host loop over B * H.
+extern "C" int clipmi_gemm_batched(void* stream, const clipmi_gemm_desc* d, int nb1, int nb2, int64_t sa1,
+                                   int64_t sa2, int64_t sb1, int64_t sb2, int64_t sc1, int64_t sc2) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
+  CLIPMI_REQUIRE(d->ab_dtype == CLIPMI_F32 && d->c_dtype == CLIPMI_F32, "batched GEMM: fp32 operands and output");
+  CLIPMI_REQUIRE((d->flags & ~CLIPMI_EPI_BETA) == 0 && d->split_k <= 1 && !d->bias_grad,
+                 "batched GEMM: no epilogue besides beta, no split-K");
+  CLIPMI_REQUIRE(nb1 >= 0 && nb2 >= 0 && (int64_t)nb1 * nb2 <= 65535, "batched GEMM: 0 <= nb1 * nb2 <= 65535");
+  CLIPMI_REQUIRE(d->A && d->B && d->C, "batched GEMM: operands");
+  if (d->M == 0 || d->N == 0 || nb1 == 0 || nb2 == 0) return CLIPMI_OK;
+  GemmP p;
+  memset(&p, 0, sizeof(p));
+  p.M = d->M; p.N = d->N; p.K = d->K;
+  p.A = d->A; p.lda = d->lda; p.B = d->B; p.ldb = d->ldb;
+  p.C = d->C; p.ldc = d->ldc; p.alpha = d->alpha; p.flags = d->flags;
+  p.k_per_split = d->K > 0 ? d->K : 1;
+  p.tiles_n = (d->N + FT - 1) / FT;
+  p.ntiles = p.tiles_n * ((d->M + FT - 1) / FT);
+  p.vec = (d->ldc % 4 == 0) && ((uintptr_t)d->C % 16 == 0) && (sc1 % 4 == 0) && (sc2 % 4 == 0);
+  p.nb2 = nb2;
+  p.bsa1 = sa1; p.bsa2 = sa2; p.bsb1 = sb1; p.bsb2 = sb2; p.bsc1 = sc1; p.bsc2 = sc2;
+  const double flops = 2.0 * d->M * d->N * d->K * nb1 * nb2;
+  ProfScope ps(s, nullptr, 0.0);
+  hipLaunchKernelGGL(gemm_f32_kernel<float>, dim3(p.ntiles, 1, nb1 * nb2), dim3(256), 0, s, p, d->a_kmajor, d->b_kmajor);
+  ps.finish("gemm_f32_batched", flops);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
@@ -1352,8 +1391,10 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     CLIPMI_REQUIRE(d->c_dtype == CLIPMI_F32 || d->c_dtype == CLIPMI_BF16 || d->c_dtype == CLIPMI_FP8, "c_dtype");
     CLIPMI_REQUIRE(d->split_k <= 1 && !d->bias_grad, "fp8: forward GEMMs only");
     const bool q8o = d->c_dtype == CLIPMI_FP8;
-    CLIPMI_REQUIRE(!q8o || (d->c_scale && d->ldc == d->N && d->N % 32 == 0 && ((uintptr_t)d->C & 7) == 0),
-                   "fp8 output: c_scale, ldc == N, N % 32 == 0, C 8-byte aligned");
+    // epilogue_q8 writes each row's e4m3 bytes as 16-B stores and a row's two scale bytes as one 16-bit store
+    CLIPMI_REQUIRE(!q8o || (d->c_scale && d->ldc == d->N && d->N % 32 == 0 && ((uintptr_t)d->C & 15) == 0 &&
+                            ((uintptr_t)d->c_scale & 1) == 0),
+                   "fp8 output: c_scale (2-byte aligned), ldc == N, N % 32 == 0, C 16-byte aligned");
     if (d->M == 0 || d->N == 0) return CLIPMI_OK;
     GemmP p;
     memset(&p, 0, sizeof(p));
@@ -1423,7 +1464,10 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.dbg = gemm_stamp_buffer();
   p.stagger = 0;
   p.first_round = num_cus();
-  if (d->force_small_tile >= 100) {  // A/B hook: 1xx the 8-wave ping-pong kernel with a first-round stagger of xx
+  if (d->force_small_tile >= 200 && d->force_small_tile < 300) {  // A/B hook: 2xx the persistent 4-wave kernel,
+    p.var = 28;                                                    // half its workgroups starting xx s_sleeps late
+    p.stagger = d->force_small_tile % 100;
+  } else if (d->force_small_tile >= 100 && d->force_small_tile < 200) {  // 1xx the 8-wave kernel, first-round stagger xx
     p.var = 9;
     p.stagger = d->force_small_tile % 100;
   } else if (d->force_small_tile >= 2) p.var = d->force_small_tile;

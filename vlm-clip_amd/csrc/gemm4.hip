@@ -434,6 +434,11 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
     w4_stage_dma<AK, BKM>(smem, p, w, wave, m0, n0, kbeg, kend, ns > 0);
     w4_stage_dma<AK, BKM>(smem + W4_STAGE, p, w, wave, m0, n0, kbeg + 64, kend, ns > 1);
   };
+  // A/B hook (force_small_tile 2xx): half of every XCD's workgroups start p.stagger s_sleep(127)s late, so
+  // with equal items per workgroup the two halves' epilogues stay offset for the whole launch
+  if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   prologue_dma(item);
   f32x4 acc[2][8][4];
   f32x4 accb[8];
@@ -901,11 +906,13 @@ const char* dispatch_w4_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, 
 
 const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg) {
   if (p.ws) {
+#ifdef CLIPMI_GEMM_EXPERIMENTS
     if (p.var == 32) {  // L2 prefetch of both operands (measured 5-8 % slower on the CLIP shapes)
       if (bg) launch_w4p<false, false, float, 0, true, true>(p, splits, s, bg);
       else launch_w4p<false, false, float, 0, false, true>(p, splits, s, bg);
       return "gemm256_wgrad_splitk";
     }
+#endif
     if (bg) launch_w4p<false, false, float, 0, true>(p, splits, s, bg);
     else launch_w4p<false, false, float, 0, false>(p, splits, s, bg);
     return "gemm256_wgrad_splitk";

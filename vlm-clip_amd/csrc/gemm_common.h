@@ -32,6 +32,10 @@ struct GemmP {
   float* bws;  // split-K with a fused bias gradient: per-split partial sums [splits][M] (no atomics)
   unsigned long long* dbg;  // diagnostic builds only: in-kernel s_memtime stamps (clipmi_gemm_stamps)
   int* dyn;  // persistent 4-wave kernel: {next-item counter, finished-workgroup counter} (dynamic queue) or null
+  // strided batch (clipmi_gemm_batched, f32 SIMT kernel only): blockIdx.z = i1 * nb2 + i2 offsets A / B / C by
+  // i1 * s?1 + i2 * s?2 elements (nb2 == 0: no batch)
+  int nb2;
+  int64_t bsa1, bsa2, bsb1, bsb2, bsc1, bsc2;
 };
 
 // host side: the stamp buffer armed by clipmi_gemm_stamps (nullptr when disarmed)
@@ -561,6 +565,17 @@ __device__ __forceinline__ void epilogue256_lds(const GemmP& p, f32x4 (&acc)[8][
 #ifndef CLIPMI_EPI_PD
 #define CLIPMI_EPI_PD 4
 #endif
+// 16-B output store of the LDS-staged epilogues; CLIPMI_STORE_NT=1 (A/B builds) makes it non-temporal
+#ifndef CLIPMI_STORE_NT
+#define CLIPMI_STORE_NT 0
+#endif
+__device__ __forceinline__ void st16_out(u32x4* p, const u32x4& v) {
+#if CLIPMI_STORE_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 // 8 bf16 packed in 4 dwords -> float (element 2i in the low half of dword i)
 __device__ __forceinline__ void unpack8(const u32x4& x, float v[8]) {
 #pragma unroll
@@ -705,11 +720,11 @@ __device__ __forceinline__ void epilogue_lds_pipe(const GemmP& p, f32x4 (&acc)[N
       const int64_t step = 8 * ld;
       if (full) {
 #pragma unroll
-        for (int it = 0; it < 8; ++it) *(u32x4*)(out + it * step) = rows[it];
+        for (int it = 0; it < 8; ++it) st16_out((u32x4*)(out + it * step), rows[it]);
       } else {
 #pragma unroll
         for (int it = 0; it < 8; ++it)
-          if (r0 + it * 8 < p.M && col < p.N) *(u32x4*)(out + it * step) = rows[it];
+          if (r0 + it * 8 < p.M && col < p.N) st16_out((u32x4*)(out + it * step), rows[it]);
       }
     };
     store_rows((bf16*)p.C, p.ldc, o);

@@ -227,6 +227,97 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
   }
 }
 
+// ---- any hidden size (the register-resident kernels above take D / 64 in {1, 2, 3, 4, 6, 8, 12, 16}):
+// one wave per row, three passes over the row (sum, centred sum of squares, normalise), the row
+// re-read from the cache.  For the modules whose width is free (peclip ContextAdapter / SharedAdapter,
+// nn.MultiheadAttention accepts any embed_dim divisible by num_heads; the adapters' LayerNorm).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_any_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
+                                                         float* mean_out, float* rstd_out, int R, int D, float eps,
+                                                         const T* pos, const T* cls, int period) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  T* xr = x + (int64_t)row * ldx;
+  const int t = pos ? row % period : 0;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    float v = (float)xr[c];
+    if (pos) {
+      v += (float)pos[(int64_t)t * D + c];
+      if (cls && t == 0) v += (float)cls[c];
+      xr[c] = (T)v;
+      v = (float)xr[c];  // the stored (rounded) sum, as the register kernels normalise it
+    }
+    s += v;
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = (float)xr[c] - mu;
+    q += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+  T* yr = y + (int64_t)row * ldy;
+  for (int c = lane; c < D; c += 64) yr[c] = (T)(((float)xr[c] - mu) * rs * (float)w[c] + (float)b[c]);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mu;
+    if (rstd_out) rstd_out[row] = rs;
+  }
+}
+
+// dx = [dres +] rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partial dgamma /
+// dbeta -> ws[blockIdx][2][D] (each wave's own LDS row pair, summed in wave order: deterministic)
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_any_kernel(const T* dy, int64_t lddy, const T* x, int64_t ldx,
+                                                         const float* mean, const float* rstd, const T* w, T* dx,
+                                                         int64_t lddx, const T* dres, int64_t ldres, float* ws, int R,
+                                                         int D) {
+  extern __shared__ float red_any[];  // [4 waves][2][D] when ws
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* pg = red_any + (int64_t)wave * 2 * D;
+  float* pb = pg + D;
+  if (ws)
+    for (int c = lane; c < D; c += 64) pg[c] = pb[c] = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const T* dyr = dy + (int64_t)row * lddy;
+    const T* xr = x + (int64_t)row * ldx;
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = lane; c < D; c += 64) {
+      const float g = (float)dyr[c] * (float)w[c];
+      s1 += g;
+      s2 += g * (((float)xr[c] - mu) * rs);
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    for (int c = lane; c < D; c += 64) {
+      const float d = (float)dyr[c], xh = ((float)xr[c] - mu) * rs;
+      float o = rs * (d * (float)w[c] - s1 - xh * s2);
+      if (dres) o += (float)dres[(int64_t)row * ldres + c];
+      dx[(int64_t)row * lddx + c] = (T)o;
+      if (ws) {
+        pg[c] += d * xh;
+        pb[c] += d;
+      }
+    }
+  }
+  if (!ws) return;
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float a = 0.f, bb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a += red_any[(int64_t)k * 2 * D + c];
+      bb += red_any[(int64_t)k * 2 * D + D + c];
+    }
+    ws[(int64_t)blockIdx.x * 2 * D + c] = a;
+    ws[(int64_t)blockIdx.x * 2 * D + D + c] = bb;
+  }
+}
+
+constexpr int LN_ANY_MAX_D = 4096;  // 4 waves x 2 x D floats of LDS = 128 KiB
+
 // out[c] (+)= sum_p ws[p*stride + c]   (deterministic second stage of every column sum)
 // block = 64 columns x 16 partial groups; fixed summation order -> bitwise reproducible
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* ws, int64_t stride, int P, int D,
@@ -527,6 +618,13 @@ void ln_bwd_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const
                      mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
 }
 
+// the widths the register-resident kernels take
+inline bool ln_fast_width(int D) {
+  if (D % 64) return false;
+  const int q = D / 64;
+  return q == 1 || q == 2 || q == 3 || q == 4 || q == 6 || q == 8 || q == 12 || q == 16;
+}
+
 // dispatch on (PS, NP) from D
 #define LN_DISPATCH(D, FN, T, ...)                                              \
   do {                                                                          \
@@ -549,9 +647,20 @@ extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ld
                                     const void* w, const void* b, float* mean, float* rstd, int R, int D,
                                     float eps, const void* pos, const void* cls, int period) {
   hipStream_t s = (hipStream_t)stream;
-  CLIPMI_REQUIRE(D % 64 == 0 && D <= 1024, "D must be a multiple of 64, <= 1024");
+  CLIPMI_REQUIRE(D >= 1 && D <= LN_ANY_MAX_D, "D must be in [1, 4096]");
   CLIPMI_REQUIRE(!pos || period > 0, "period");
   if (R == 0) return CLIPMI_OK;
+  if (!ln_fast_width(D)) {  // any other width: the one-wave-per-row kernel
+    const dim3 g((R + 3) / 4);
+    if (dtype == CLIPMI_BF16)
+      hipLaunchKernelGGL(ln_fwd_any_kernel<bf16>, g, dim3(256), 0, s, (bf16*)x, ldx, (bf16*)y, ldy, (const bf16*)w,
+                         (const bf16*)b, mean, rstd, R, D, eps, (const bf16*)pos, (const bf16*)cls, period);
+    else
+      hipLaunchKernelGGL(ln_fwd_any_kernel<float>, g, dim3(256), 0, s, (float*)x, ldx, (float*)y, ldy, (const float*)w,
+                         (const float*)b, mean, rstd, R, D, eps, (const float*)pos, (const float*)cls, period);
+    CLIPMI_CHECK_LAUNCH();
+    return CLIPMI_OK;
+  }
   if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_fwd_launch, bf16, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
   else LN_DISPATCH(D, ln_fwd_launch, float, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
   CLIPMI_CHECK_LAUNCH();
@@ -584,16 +693,30 @@ extern "C" int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int
                                     const void* dres, int64_t ldres, float* dw, float* db, int beta_wb,
                                     void* ws, int64_t ws_bytes, int R, int D) {
   hipStream_t s = (hipStream_t)stream;
-  CLIPMI_REQUIRE(D % 64 == 0 && D <= 1024, "D must be a multiple of 64, <= 1024");
+  CLIPMI_REQUIRE(D >= 1 && D <= LN_ANY_MAX_D, "D must be in [1, 4096]");
   if (R == 0) return CLIPMI_OK;
   int nb = (R + 3) / 4;
   if (nb > 1024) nb = 1024;
   float* wsf = (dw || db) ? (float*)ws : nullptr;
   if (wsf) CLIPMI_REQUIRE(ws_bytes >= (int64_t)nb * 2 * D * 4, "layernorm_bwd workspace too small");
-  if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
-  else LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  if (!ln_fast_width(D)) {
+    const size_t lds = wsf ? (size_t)4 * 2 * D * 4 : 0;
+    if (dtype == CLIPMI_BF16) {
+      (void)lds_optin((const void*)ln_bwd_any_kernel<bf16>, (int)lds);
+      hipLaunchKernelGGL(ln_bwd_any_kernel<bf16>, dim3(nb), dim3(256), lds, s, (const bf16*)dy, lddy, (const bf16*)x, ldx,
+                         mean, rstd, (const bf16*)w, (bf16*)dx, lddx, (const bf16*)dres, ldres, wsf, R, D);
+    } else {
+      (void)lds_optin((const void*)ln_bwd_any_kernel<float>, (int)lds);
+      hipLaunchKernelGGL(ln_bwd_any_kernel<float>, dim3(nb), dim3(256), lds, s, (const float*)dy, lddy, (const float*)x,
+                         ldx, mean, rstd, (const float*)w, (float*)dx, lddx, (const float*)dres, ldres, wsf, R, D);
+    }
+  } else if (dtype == CLIPMI_BF16) {
+    LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  } else {
+    LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  }
   CLIPMI_CHECK_LAUNCH();
-  if (((uintptr_t)wsf & 15) != 0) {
+  if (((uintptr_t)wsf & 15) != 0 || D % 4 != 0) {
     if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
     if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
   } else if (dw && db)
