@@ -90,7 +90,9 @@ def synthetic_batch(cfg, B, rank, device, seed=1234):
 FAMILIES = {
     "gemm256_fwd_dgrad": ["gemm256_fwd_bias", "gemm256_fwd_bias_resid", "gemm256_fwd_bias_qgelu_pre",
                           "gemm256_fwd_bias_qgelu_dact", "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad",
-                          "gemm256_dgrad_dqgelu", "gemm256_dgrad_mulaux"],
+                          "gemm256_dgrad_dqgelu", "gemm256_dgrad_mulaux",
+                          # fp32 residual stream: out-projection / fc2 write the fp32 sum (round 5)
+                          "gemm256_fwd_bias_resid_f32", "gemm256_fwd_bias_f32", "gemm256_fwd_f32"],
     "gemm256_wgrad": ["gemm256_wgrad_splitk", "gemm256_wgrad"],
     "attention": ["attn_fwd", "attn_bwd"],
     "gemm_fp8": ["gemm_fp8_fwd_bias", "gemm_fp8_fwd_bias_resid", "gemm_fp8_fwd_bias_qgelu",
@@ -105,17 +107,21 @@ TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r04_traffic_fwd_dgrad.json",
                  "attention": "profiles/r02_traffic_attention.json"}
 
 
-def vision_gemm_shapes(cfg, B, train):
+def vision_gemm_shapes(cfg, B, train, resid32=False):
     """(M, N, K, extra_bytes) of the vision tower's 256-kernel launches on the caller's stream,
-    per step, in the families above; extra = epilogue operands/outputs beyond A, B and C once."""
+    per step, in the families above; extra = epilogue operands/outputs beyond A, B and C once
+    (counted at 2 bytes per element).  resid32: the bf16 mode's fp32 residual stream (round 5) --
+    the patch embedding, out-projection and fc2 write fp32 (+2 B per output element) and the
+    latter two read the fp32 residual (4 B per element)."""
     v = cfg.vision_config
     R = B * ((v.image_size // v.patch_size) ** 2 + 1)
     D, F = v.hidden_size, v.intermediate_size
     Kp = 3 * v.patch_size ** 2
     Kp = (Kp + 63) // 64 * 64 if Kp % 8 else Kp
-    fwd = [(R, D, Kp, 0)]
+    rx = R * D * 6 if resid32 else R * D * 2  # residual read (+ the wider sum written)
+    fwd = [(R, D, Kp, R * D * 2 if resid32 else 0)]
     for _ in range(v.num_hidden_layers):
-        fwd += [(R, 3 * D, D, 0), (R, D, D, R * D * 2), (R, F, D, R * F * 2 if train else 0), (R, D, F, R * D * 2)]
+        fwd += [(R, 3 * D, D, 0), (R, D, D, rx), (R, F, D, R * F * 2 if train else 0), (R, D, F, rx)]
     dgrad, wgrad = [], []
     if train:
         for _ in range(v.num_hidden_layers):
@@ -125,10 +131,10 @@ def vision_gemm_shapes(cfg, B, train):
     return fwd + dgrad, wgrad
 
 
-def algorithmic_bytes(cfg, B, train):
+def algorithmic_bytes(cfg, B, train, resid32=False):
     """Mean compulsory HBM bytes per launch of each GEMM family (bf16 operands read once, output
     written once: bf16 for forward/dgrad, fp32 gradient for wgrad), vision tower launches."""
-    fd, wg = vision_gemm_shapes(cfg, B, train)
+    fd, wg = vision_gemm_shapes(cfg, B, train, resid32)
     out = {"gemm256_fwd_dgrad": sum((M * K + N * K + M * N) * 2 + x for M, N, K, x in fd) / len(fd)}
     if wg:
         out["gemm256_wgrad"] = sum(K * (M + N) * 2 + M * N * 4 for M, N, K in wg) / len(wg)
@@ -250,7 +256,7 @@ def self_launch(args):
     return subprocess.run(cmd, env=env).returncode
 
 
-def family_roofline(name, launches, cfg, B, train):
+def family_roofline(name, launches, cfg, B, train, resid32=False):
     """launches: [(ms, flops)] of one family on the caller's stream inside the timed steps."""
     if not launches:
         return None
@@ -258,7 +264,7 @@ def family_roofline(name, launches, cfg, B, train):
     tot_fl = sum(f for _, f in launches)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
     peak = PEAKS.get(name, PEAK_BF16_TFLOPS)
-    alg = algorithmic_bytes(cfg, B, train).get(name)
+    alg = algorithmic_bytes(cfg, B, train, resid32).get(name)
     res = {"bound": "mfma", "kernel": name, "labels": {**FAMILIES, **FAMILIES_FP32}[name], "launches": len(launches),
            "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
            "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
@@ -396,7 +402,8 @@ def main():
                 per_fam[name].append((ms[i], fl[i]))
     roofs = {}
     for name in fams:
-        r = family_roofline(name, per_fam[name], cfg, args.batch, not adapters)
+        r = family_roofline(name, per_fam[name], cfg, args.batch, not adapters,
+                            resid32=bool(getattr(model._rt, "resid32", False)))
         if r is not None:
             r["ms_per_step_caller_stream"] = round(sum(m for m, _ in per_fam[name]) / args.steps, 2)
             roofs[name] = r

@@ -118,6 +118,11 @@ int clipmi_quant_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, int6
 int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy, const void* w,
                          const void* b, float* mean, float* rstd, int R, int D, float eps, const void* pos,
                          const void* cls, int period);
+/* The same with the input x (and pos / cls) in x_dtype and y, w, b in dtype: x_dtype == dtype, or an fp32 x
+ * normalised into a bf16 y (the bf16 mode's fp32 residual stream -> the next GEMM's bf16 operand). */
+int clipmi_layernorm_fwd2(void* stream, int x_dtype, int dtype, void* x, int64_t ldx, void* y, int64_t ldy,
+                          const void* w, const void* b, float* mean, float* rstd, int R, int D, float eps,
+                          const void* pos, const void* cls, int period);
 /* The same LayerNorm (bf16 x, no embedding add) with its output written as MXFP8, quantised
  * from the fp32 result as clipmi_quant_mxfp8 does: q8 [R, D] e4m3, s8 [R, D/32] E8M0.  Feeds the
  * fp8 tower GEMMs (BASELINE config 5) without a bf16 round trip. D % 256 == 0, D <= 1024. */
@@ -128,6 +133,11 @@ int64_t clipmi_layernorm_bwd_ws(int R, int D);
 int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                          const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                          int64_t ldres, float* dw, float* db, int beta_wb, void* ws, int64_t ws_bytes, int R, int D);
+/* The same with x in x_dtype (fp32 residual stream) and dy, dx, dres, w in dtype (bf16 gradients). */
+int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const void* dy, int64_t lddy, const void* x,
+                          int64_t ldx, const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx,
+                          const void* dres, int64_t ldres, float* dw, float* db, int beta_wb, void* ws,
+                          int64_t ws_bytes, int R, int D);
 /* out[n] (+)= sum_r x[r][n]  (bias gradients of every Linear on the path) */
 int64_t clipmi_colsum_ws(int R, int N);
 int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, int N, float* out, int beta, void* ws,
@@ -237,6 +247,11 @@ typedef struct clipmi_encoder_desc {
   const clipmi_layer_w8* layers8; /* [L], CLIPMI_FP8 only */
   void* q8;                       /* CLIPMI_FP8: MXFP8 activation scratch, align256(R*D) + R*F bytes (R = B*N) */
   void* s8;                       /* CLIPMI_FP8: its block scales, align256(R*D/32) + R*F/32 bytes */
+  /* dtype CLIPMI_BF16 only: the residual stream in fp32 -- act[l].x_in, act[l].h and x_out are fp32
+   * (LayerNorms read them as fp32, the out-projection / fc2 epilogues add and write fp32), every GEMM
+   * operand stays bf16.  The reference is fp32 end to end (trainer.py:81-99); rounding the residual sum
+   * to bf16 at each of the 2L residual adds was the largest bf16-mode error (profiles/r05_bf16_error_sources.log). */
+  int resid_f32;
 } clipmi_encoder_desc;
 int clipmi_encoder_fwd(void* stream, const clipmi_encoder_desc* d);
 int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d);

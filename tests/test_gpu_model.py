@@ -668,10 +668,12 @@ def test_config3_full_size_matches_torch_oracle():
     contrastive loss) against the oracle (oracle/clip_ref.py, pinned to the reference by the goldens)
     run by PyTorch on the same GPU, weights and batch: (1) clipmi fp32 vs the oracle in fp32 --
     loss, logits and every parameter gradient (relative L2 of the difference); (2) clipmi bf16 vs the
-    same fp32 oracle, measured against PyTorch's own bf16 run of the oracle (FlashAttention's test
-    rule: the bf16 kernels' error may be at most a small multiple of a plain bf16 implementation's).
-    Tensors with a negligible gradient (k-projection biases: zero by softmax shift invariance) are
-    skipped."""
+    same fp32 oracle, measured against PyTorch's mixed-precision run of the oracle (torch.autocast
+    bf16: bf16 GEMM operands with fp32 accumulation, fp32 LayerNorm / softmax / loss, fp32 residual
+    stream and master weights): clipmi's max |dlogit| and every tensor's gradient error at most 1.5x
+    the mixed-precision run's, and max |dlogit| <= 0.10 at logit scale 100.  PyTorch's all-bf16 run is
+    printed beside them.  Tensors with a negligible gradient (k-projection biases: zero by softmax
+    shift invariance) are skipped."""
     from oracle import clip_ref as R
     res, params = {}, None
     for precision in ("fp32", "bf16"):
@@ -688,9 +690,10 @@ def test_config3_full_size_matches_torch_oracle():
             params = {n[5:]: p.detach().clone() for n, p in m.named_parameters()}
         del m, out
         torch.cuda.empty_cache()
-    for dt, tag in ((torch.float32, "torch32"), (torch.bfloat16, "torch16")):
+    for dt, tag, amp in ((torch.float32, "torch32", False), (torch.float32, "torchamp", True),
+                         (torch.bfloat16, "torch16", False)):
         p = {k: v.to(dt).clone().requires_grad_(True) for k, v in params.items()}
-        with torch.device("cuda"):
+        with torch.device("cuda"), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = R.clip_with_adapters_forward(b, p, cfg)
         out["loss"].backward()
         torch.cuda.synchronize()
@@ -701,26 +704,26 @@ def test_config3_full_size_matches_torch_oracle():
     lref, zref, gref = res["torch32"]
     nmax = max(float(v.norm()) for v in gref.values())
     names = [n for n, a in gref.items() if "k_proj.bias" not in n and float(a.norm()) >= 1e-4 * nmax]
-    rel = {k: {n: float((res[k][2][n] - gref[n]).norm() / gref[n].norm()) for n in names}
-           for k in ("fp32", "bf16", "torch16")}
-    dz = {k: float((res[k][1] - zref).abs().max()) for k in ("fp32", "bf16", "torch16")}
-    dl = {k: abs(res[k][0] - lref) for k in ("fp32", "bf16", "torch16")}
-    ratio = sorted(((rel["bf16"][n] / max(rel["torch16"][n], 1e-6), n) for n in names), reverse=True)
+    kinds = ("fp32", "bf16", "torchamp", "torch16")
+    rel = {k: {n: float((res[k][2][n] - gref[n]).norm() / gref[n].norm()) for n in names} for k in kinds}
+    dz = {k: float((res[k][1] - zref).abs().max()) for k in kinds}
+    dl = {k: abs(res[k][0] - lref) for k in kinds}
+    ratio = sorted(((rel["bf16"][n] / max(rel["torchamp"][n], 1e-6), n) for n in names), reverse=True)
     r32 = sorted(((v, n) for n, v in rel["fp32"].items()), reverse=True)
     w32 = r32[0]
     print(f"\n[config 3 B=1024 vs torch fp32 oracle] {len(names)} tensors; |dloss| {dl}; max|dlogit| {dz}\n"
           f"  clipmi fp32: worst grad rel-L2 {r32[:3]}; median {r32[len(r32) // 2]}\n"
           f"  clipmi bf16: worst rel-L2 {max((v, n) for n, v in rel['bf16'].items())}; "
-          f"torch bf16 worst {max((v, n) for n, v in rel['torch16'].items())}\n"
-          f"  worst bf16 ratio clipmi/torch {ratio[:4]}; median {ratio[len(ratio) // 2]}")
+          f"torch amp worst {max((v, n) for n, v in rel['torchamp'].items())}; "
+          f"torch all-bf16 worst {max((v, n) for n, v in rel['torch16'].items())}\n"
+          f"  worst bf16 ratio clipmi/amp {ratio[:4]}; median {ratio[len(ratio) // 2]}")
     assert len(names) > 150
     assert dl["fp32"] < 1e-4 and dz["fp32"] < 1e-3, (dl, dz)
     # fp32: summation order over R = 201,728 rows (bias / weight gradients are sums over every token,
     # with heavy cancellation) -- measured worst 5.1e-3 (last layer's v-projection bias)
     assert w32[0] < 1e-2, w32
     assert r32[len(r32) // 2][0] < 2e-3, r32[len(r32) // 2]  # measured median 7.4e-4
-    # bf16: measured |dloss| 3.6e-4 (torch bf16 4.5e-3), max|dlogit| 0.147 (torch 0.190); per tensor
-    # clipmi's bf16 error is at most 0.30x PyTorch's bf16 error (median 0.018x)
-    assert dl["bf16"] < 0.02 and dz["bf16"] < LOGIT_TOL["bf16"], (dl, dz)
-    assert dl["bf16"] <= dl["torch16"] and dz["bf16"] <= dz["torch16"], (dl, dz)
-    assert ratio[0][0] < 1.0, ratio[0]
+    # bf16 (fp32 residual stream since round 5) against PyTorch's mixed precision
+    assert dl["bf16"] < 0.02, dl
+    assert dz["bf16"] <= 0.10 and dz["bf16"] <= 1.5 * dz["torchamp"], dz
+    assert ratio[0][0] <= 1.5, ratio[:4]

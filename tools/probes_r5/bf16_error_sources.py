@@ -23,7 +23,8 @@ from clipmi import CLIPWithAdapters, synth  # noqa: E402
 from oracle import clip_ref as R  # noqa: E402
 
 B = int(os.environ.get("B", "1024"))
-dev = "cuda"
+dev = os.environ.get("DEV", "cuda")  # DEV=cpu PRESET=tiny: a dry run of the emulation code on the host
+PRESET = os.environ.get("PRESET", "B/16")
 
 
 def rb(x):
@@ -76,7 +77,7 @@ class Emu:
         t = cfg.text_config
         x = self.res(p["text_model.embeddings.token_embedding.weight"][b["input_ids"]] +
                      p["text_model.embeddings.position_embedding.weight"][: b["input_ids"].shape[1]])
-        mask = R.causal_padding_mask(b["attention_mask"].cpu(), torch.float32).to(dev)
+        mask = R.causal_padding_mask(b["attention_mask"], torch.float32)
         for i in range(t.num_hidden_layers):
             x = self.layer(x, p, f"text_model.encoder.layers.{i}", t.num_attention_heads, t.layer_norm_eps, mask)
         x = self.ln(x, p["text_model.final_layer_norm.weight"], p["text_model.final_layer_norm.bias"], t.layer_norm_eps)
@@ -94,17 +95,22 @@ class Emu:
         return R.contrastive(tf, imf, p["logit_scale"])
 
 
-m = CLIPWithAdapters("B/16", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
-                     freeze_clip=False, device=dev, precision="bf16", fast_init=True)
-cfg = m.config
-bn = synth.synthetic_batch(cfg, B, seed=1234)
-b = {k: torch.from_numpy(v).to(dev) for k, v in bn.items()}
+from clipmi import config as C  # noqa: E402
 with torch.no_grad():
-    out = m(**b, return_loss=True)
-    res = {"clipmi": (out["loss"].item(), out["logits_per_text"].float())}
-    params = {n[5:]: p.detach().float().clone() for n, p in m.named_parameters()}
-    del m, out
-    torch.cuda.empty_cache()
+    if dev == "cuda":
+        m = CLIPWithAdapters(PRESET, use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                             freeze_clip=False, device=dev, precision="bf16", fast_init=True)
+        cfg = m.config
+        b = {k: torch.from_numpy(v).to(dev) for k, v in synth.synthetic_batch(cfg, B, seed=1234).items()}
+        out = m(**b, return_loss=True)
+        res = {"clipmi": (out["loss"].item(), out["logits_per_text"].float())}
+        params = {n[5:]: p.detach().float().clone() for n, p in m.named_parameters()}
+        del m, out
+        torch.cuda.empty_cache()
+    else:
+        cfg = C.resolve(PRESET)
+        b = {k: torch.from_numpy(v) for k, v in synth.synthetic_batch(cfg, B, seed=1234).items()}
+        params, res = R.to_torch(synth.clip_state_dict(cfg, seed=0)), {}
     with torch.device(dev):
         o = R.clip_with_adapters_forward(b, params, cfg)
     res["fp32"] = (o["loss"].item(), o["logits_per_text"].float())

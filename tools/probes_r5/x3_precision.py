@@ -19,7 +19,8 @@ from clipmi import CLIPWithAdapters, synth  # noqa: E402
 from oracle import clip_ref as R  # noqa: E402
 
 B = int(os.environ.get("B", "1024"))
-dev = "cuda"
+dev = os.environ.get("DEV", "cuda")  # DEV=cpu PRESET=tiny: a dry run of the emulation code on the host
+PRESET = os.environ.get("PRESET", "B/16")
 
 
 def rb(x):
@@ -78,7 +79,7 @@ class X3:
         x = p["text_model.embeddings.token_embedding.weight"][b["input_ids"]] + \
             p["text_model.embeddings.position_embedding.weight"][: b["input_ids"].shape[1]]
         x = self.st(x)
-        mask = R.causal_padding_mask(b["attention_mask"].cpu(), torch.float32).to(dev)
+        mask = R.causal_padding_mask(b["attention_mask"], torch.float32)
         for i in range(t.num_hidden_layers):
             x = self.layer(x, p, f"text_model.encoder.layers.{i}", t.num_attention_heads, t.layer_norm_eps, mask)
         x = self.st(R.layer_norm(x, p["text_model.final_layer_norm.weight"], p["text_model.final_layer_norm.bias"],
@@ -100,17 +101,22 @@ class X3:
         return R.contrastive(tf, imf, p["logit_scale"])
 
 
-m = CLIPWithAdapters("B/16", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
-                     freeze_clip=False, device=dev, precision="fp32", fast_init=True)
-cfg = m.config
-bn = synth.synthetic_batch(cfg, B, seed=1234)
-b = {k: torch.from_numpy(v).to(dev) for k, v in bn.items()}
+from clipmi import config as C  # noqa: E402
 with torch.no_grad():
-    out = m(**b, return_loss=True)
-    res = {"clipmi32": (out["loss"].item(), out["logits_per_text"].float())}
-    params = {n[5:]: p.detach().float().clone() for n, p in m.named_parameters()}
-    del m, out
-    torch.cuda.empty_cache()
+    if dev == "cuda":
+        m = CLIPWithAdapters(PRESET, use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                             freeze_clip=False, device=dev, precision="fp32", fast_init=True)
+        cfg = m.config
+        b = {k: torch.from_numpy(v).to(dev) for k, v in synth.synthetic_batch(cfg, B, seed=1234).items()}
+        out = m(**b, return_loss=True)
+        res = {"clipmi32": (out["loss"].item(), out["logits_per_text"].float())}
+        params = {n[5:]: p.detach().float().clone() for n, p in m.named_parameters()}
+        del m, out
+        torch.cuda.empty_cache()
+    else:
+        cfg = C.resolve(PRESET)
+        b = {k: torch.from_numpy(v) for k, v in synth.synthetic_batch(cfg, B, seed=1234).items()}
+        params, res = R.to_torch(synth.clip_state_dict(cfg, seed=0)), {}
     torch.backends.cuda.matmul.allow_tf32 = False
     with torch.device(dev):
         o = R.clip_with_adapters_forward(b, params, cfg)
@@ -119,7 +125,8 @@ with torch.no_grad():
         with torch.device(dev):
             o = e.forward(b, params, cfg)
         res[name] = (o["loss"].item(), o["logits_per_text"].float())
-        torch.cuda.empty_cache()
+        if dev == 'cuda':
+            torch.cuda.empty_cache()
 l0, z0 = res["fp32"]
 for k, (l, z) in res.items():
     d = (z - z0).abs()

@@ -124,6 +124,8 @@ class CLIPWithAdapters(nn.Module):
                                                   for i in range(shared_adapter_layers)])
         self._rt = _Runtime(self.clip, dtype)
         self._rt.fp8 = precision == "fp8"
+        # bf16 mode: the towers' residual stream in fp32 (engine resid_f32; profiles/r05_bf16_error_sources.log)
+        self._rt.resid32 = precision == "bf16"
         if freeze_clip:
             self._freeze_clip_parameters()
 

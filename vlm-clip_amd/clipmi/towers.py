@@ -57,7 +57,8 @@ class EncoderDesc(ctypes.Structure):
                 ("L", c_int), ("eps", c_float), ("causal", c_int), ("attention_mask", c_vp),
                 ("layers", ctypes.POINTER(LayerW)), ("grads", ctypes.POINTER(LayerG)),
                 ("act", ctypes.POINTER(LayerAct)), ("x_out", c_vp), ("workspace", c_vp),
-                ("workspace_bytes", c_i64), ("layers8", ctypes.POINTER(LayerW8)), ("q8", c_vp), ("s8", c_vp)]
+                ("workspace_bytes", c_i64), ("layers8", ctypes.POINTER(LayerW8)), ("q8", c_vp), ("s8", c_vp),
+                ("resid_f32", c_int)]
 
 
 P = ctypes.POINTER
@@ -67,6 +68,10 @@ _lib.declare("clipmi_encoder_bwd_ws", [P(EncoderDesc)], c_i64)
 _lib.declare("clipmi_encoder_bwd_layers", [c_vp, P(EncoderDesc), c_vp, c_int, c_int])
 _lib.declare("clipmi_layernorm_fwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                       c_float, c_vp, c_vp, c_int])
+_lib.declare("clipmi_layernorm_fwd2", [c_vp, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
+                                       c_int, c_float, c_vp, c_vp, c_int])
+_lib.declare("clipmi_layernorm_bwd2", [c_vp, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                       c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
 _lib.declare("clipmi_layernorm_bwd_ws", [c_int, c_int], c_i64)
 _lib.declare("clipmi_layernorm_bwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
                                       c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
@@ -213,14 +218,16 @@ class Encoder:
     def grads(self):
         return self._table(LayerG, self.arena.grad)
 
-    def alloc(self, B, N, dtype, device, train):
-        """Activation storage: per-layer for training, one shared set for inference."""
+    def alloc(self, B, N, dtype, device, train, resid32=False):
+        """Activation storage: per-layer for training, one shared set for inference.  resid32: the
+        residual stream (x_in, h) in fp32 (the bf16 mode's fp32 residual stream)."""
         t = self.t
         R, D, F, H, L = B * N, t.hidden_size, t.intermediate_size, t.num_attention_heads, t.num_hidden_layers
         es = 2 if dtype == torch.bfloat16 else 4
+        xs = 4 if resid32 else es
         al = lambda n: (n + 255) // 256 * 256  # noqa: E731
-        parts = [("x_in", R * D * es), ("ln1", R * D * es), ("qkv", R * 3 * D * es), ("o", R * D * es),
-                 ("h", R * D * es), ("ln2", R * D * es), ("act", R * F * es),
+        parts = [("x_in", R * D * xs), ("ln1", R * D * es), ("qkv", R * 3 * D * es), ("o", R * D * es),
+                 ("h", R * D * xs), ("ln2", R * D * es), ("act", R * F * es),
                  ("mean1", R * 4), ("rstd1", R * 4), ("lse", B * H * N * 4), ("mean2", R * 4), ("rstd2", R * 4)]
         if train:
             parts.append(("pre", R * F * es))
@@ -263,10 +270,11 @@ class Encoder:
         self._wcache["w8"] = (key, tab, keep)
         return tab
 
-    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None, fp8=False):
+    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None, fp8=False, resid32=False):
         t = self.t
         d = EncoderDesc()
         d.dtype, d.B, d.N, d.D, d.F = dcode(dtype), B, N, t.hidden_size, t.intermediate_size
+        d.resid_f32 = int(resid32 and not fp8)
         if fp8:  # bf16 activations, MXFP8 GEMMs (forward only)
             d.dtype = _lib.FP8
             d.layers8 = self.weights8()
@@ -366,23 +374,31 @@ class VisionTowerFn(torch.autograd.Function):
             im2col_uint8(px, X, v.image_size, Pp)
         else:
             call("clipmi_im2col", s, dc, P_(px), P_(X), B, v.num_channels, H, Pp, Kp)
-        h0 = torch.empty(R, D, dtype=dtype, device=dev)
+        # the fp32 residual stream (bf16 mode): the patch product, the embedding sum and pre_layrnorm in
+        # fp32 (fp32 master position / class / LN parameters), so layer 0's input is fp32 like every
+        # later layer's; the patch GEMM's operands stay bf16
+        fp8 = rt.fp8 and not train
+        r32 = getattr(rt, "resid32", False) and not fp8
+        xdtype = torch.float32 if r32 else dtype
+        ebuf = arena.data if r32 else wbuf
+        h0 = torch.empty(R, D, dtype=xdtype, device=dev)
         Wp = arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kc)
         if Kp != Kc:
             Wp = torch.nn.functional.pad(Wp, (0, Kp - Kc))
         K.gemm(R, D, Kp, X, Kp, True, Wp, Kp, True, h0, D)
-        buf, acts = rt.venc.alloc(B, N, dtype, dev, train)
+        buf, acts = rt.venc.alloc(B, N, dtype, dev, train, resid32=r32)
         stats0 = torch.empty(2, R, dtype=torch.float32, device=dev)
-        call("clipmi_layernorm_fwd", s, dc, P_(h0), D, acts[0].x_in, D,
-             arena.ptr("vision_model.pre_layrnorm.weight", wbuf), arena.ptr("vision_model.pre_layrnorm.bias", wbuf),
+        call("clipmi_layernorm_fwd", s, dcode(xdtype), P_(h0), D, acts[0].x_in, D,
+             arena.ptr("vision_model.pre_layrnorm.weight", ebuf), arena.ptr("vision_model.pre_layrnorm.bias", ebuf),
              P_(stats0[0]), P_(stats0[1]), R, D, v.layer_norm_eps,
-             arena.ptr("vision_model.embeddings.position_embedding.weight", wbuf),
-             arena.ptr("vision_model.embeddings.class_embedding", wbuf), N)
-        out = torch.empty(B, N, D, dtype=dtype, device=dev)
-        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None, fp8=rt.fp8 and not train)
+             arena.ptr("vision_model.embeddings.position_embedding.weight", ebuf),
+             arena.ptr("vision_model.embeddings.class_embedding", ebuf), N)
+        out = torch.empty(B, N, D, dtype=xdtype, device=dev)
+        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None, fp8=fp8, resid32=r32)
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
         if train:
             ctx.rt, ctx.B, ctx.buf, ctx.acts, ctx.X, ctx.h0, ctx.stats0 = rt, B, buf, acts, X, h0, stats0
+            ctx.r32 = r32
         else:
             del buf
         return out
@@ -399,17 +415,18 @@ class VisionTowerFn(torch.autograd.Function):
         arena.prepare_grads()
         wbuf = _wbuf(arena, dtype)
         dx = dout.to(dtype).contiguous().clone()
-        d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads())
+        d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads(), resid32=ctx.r32)
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
         hook = _grad_hook(rt)
         rt.venc.backward(s, d, dx.data_ptr(), hook)
-        # pre_layrnorm backward -> gradient of the embedding sum h0
+        # pre_layrnorm backward -> gradient of the embedding sum h0 (h0 fp32 with the fp32 residual stream;
+        # the gradients stay in the activation dtype)
         dh0 = torch.empty(R, D, dtype=dtype, device=dev)
         lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
         g = arena.grad
-        call("clipmi_layernorm_bwd", s, dc, P_(dx), D, P_(ctx.h0), D, P_(ctx.stats0[0]), P_(ctx.stats0[1]),
-             arena.ptr("vision_model.pre_layrnorm.weight", wbuf), P_(dh0), D, None, 0,
+        call("clipmi_layernorm_bwd2", s, dcode(ctx.h0.dtype), dc, P_(dx), D, P_(ctx.h0), D, P_(ctx.stats0[0]),
+             P_(ctx.stats0[1]), arena.ptr("vision_model.pre_layrnorm.weight", wbuf), P_(dh0), D, None, 0,
              arena.ptr("vision_model.pre_layrnorm.weight", g), arena.ptr("vision_model.pre_layrnorm.bias", g), 1,
              P_(lws), lws.numel(), R, D)
         Kp, Kc = ctx.X.shape[1], v.num_channels * v.patch_size ** 2
@@ -460,22 +477,26 @@ class TextTowerFn(torch.autograd.Function):
         s = K.stream()
         dc = dcode(dtype)
         wbuf = _wbuf(arena, dtype)
-        buf, acts = rt.tenc.alloc(B, S, dtype, dev, train)
+        fp8 = rt.fp8 and not train
+        r32 = getattr(rt, "resid32", False) and not fp8  # the fp32 residual stream (bf16 mode)
+        xdtype = torch.float32 if r32 else dtype
+        buf, acts = rt.tenc.alloc(B, S, dtype, dev, train, resid32=r32)
         bad = rt.bad_flag
-        call("clipmi_text_embed", s, dc, P_(ids), arena.ptr("text_model.embeddings.token_embedding.weight", wbuf),
-             arena.ptr("text_model.embeddings.position_embedding.weight", wbuf), acts[0].x_in, R, S, D, t.vocab_size,
+        ebuf = arena.data if r32 else wbuf  # fp32 token / position embeddings into the fp32 stream
+        call("clipmi_text_embed", s, dcode(xdtype), P_(ids), arena.ptr("text_model.embeddings.token_embedding.weight", ebuf),
+             arena.ptr("text_model.embeddings.position_embedding.weight", ebuf), acts[0].x_in, R, S, D, t.vocab_size,
              P_(bad))
-        xL = torch.empty(R, D, dtype=dtype, device=dev)
-        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask, fp8=rt.fp8 and not train)
+        xL = torch.empty(R, D, dtype=xdtype, device=dev)
+        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask, fp8=fp8, resid32=r32)
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
         out = torch.empty(B, S, D, dtype=dtype, device=dev)
         stats = torch.empty(2, R, dtype=torch.float32, device=dev)
-        call("clipmi_layernorm_fwd", s, dc, P_(xL), D, P_(out), D, arena.ptr("text_model.final_layer_norm.weight", wbuf),
-             arena.ptr("text_model.final_layer_norm.bias", wbuf), P_(stats[0]), P_(stats[1]), R, D, t.layer_norm_eps,
-             None, None, 0)
+        call("clipmi_layernorm_fwd2", s, dcode(xdtype), dc, P_(xL), D, P_(out), D,
+             arena.ptr("text_model.final_layer_norm.weight", wbuf), arena.ptr("text_model.final_layer_norm.bias", wbuf),
+             P_(stats[0]), P_(stats[1]), R, D, t.layer_norm_eps, None, None, 0)
         if train:
             ctx.rt, ctx.B, ctx.S, ctx.buf, ctx.acts = rt, B, S, buf, acts
-            ctx.ids, ctx.mask, ctx.xL, ctx.stats = ids, mask, xL, stats
+            ctx.ids, ctx.mask, ctx.xL, ctx.stats, ctx.r32 = ids, mask, xL, stats, r32
         return out
 
     @staticmethod
@@ -493,11 +514,11 @@ class TextTowerFn(torch.autograd.Function):
         dy = dout.to(dtype).contiguous()
         dx = torch.empty(R, D, dtype=dtype, device=dev)
         lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
-        call("clipmi_layernorm_bwd", s, dc, P_(dy), D, P_(ctx.xL), D, P_(ctx.stats[0]), P_(ctx.stats[1]),
-             arena.ptr("text_model.final_layer_norm.weight", wbuf), P_(dx), D, None, 0,
+        call("clipmi_layernorm_bwd2", s, dcode(ctx.xL.dtype), dc, P_(dy), D, P_(ctx.xL), D, P_(ctx.stats[0]),
+             P_(ctx.stats[1]), arena.ptr("text_model.final_layer_norm.weight", wbuf), P_(dx), D, None, 0,
              arena.ptr("text_model.final_layer_norm.weight", g), arena.ptr("text_model.final_layer_norm.bias", g), 1,
              P_(lws), lws.numel(), R, D)
-        d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads())
+        d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads(), resid32=ctx.r32)
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
         hook = _grad_hook(rt)
@@ -598,13 +619,17 @@ class PoolProjFn(torch.autograd.Function):
         E = W.shape[0]
         if W.shape[1] != D:  # F.linear's error for the reference's text_projection(x) (model_m.py:103)
             raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({B}x{D} and {W.shape[1]}x{E})")
-        hc = h.to(dtype).contiguous()
-        pooled = torch.empty(B, D, dtype=dtype, device=dev)
-        call("clipmi_gather_rows", s, dc, P_(hc), P_(idx), B, S, D, P_(pooled))
+        # gather the pooled rows in h's own dtype (the vision tower's fp32 residual stream), then cast
+        # the B rows (not the whole [B, S, D] tensor) to the GEMM operand dtype
+        hd = h.dtype if h.dtype in (torch.float32, torch.bfloat16) else dtype
+        hc = h.to(hd).contiguous()
+        pooled = torch.empty(B, D, dtype=hd, device=dev)
+        call("clipmi_gather_rows", s, dcode(hd), P_(hc), P_(idx), B, S, D, P_(pooled))
+        pooled = pooled.to(dtype)
         out = torch.empty(B, E, dtype=torch.float32, device=dev)
         K.gemm(B, E, D, pooled, D, True, W, D, True, out, E)
         ctx.save = (pooled, idx)
-        ctx.rt, ctx.wname, ctx.shape = runtime, wname, (B, S, D)
+        ctx.rt, ctx.wname, ctx.shape, ctx.hdtype = runtime, wname, (B, S, D), hd
         return out
 
     @staticmethod
@@ -629,8 +654,10 @@ class PoolProjFn(torch.autograd.Function):
             K.gemm(E, D, B, d, E, False, pooled, D, False, arena.view(ctx.wname, arena.grad), D, flags=_lib.EPI_BETA)
         dpooled = torch.empty(B, D, dtype=dtype, device=dev)
         K.gemm(B, D, E, d, E, True, W, D, False, dpooled, D)
-        dh = torch.zeros(B, S, D, dtype=dtype, device=dev)
-        call("clipmi_scatter_rows", s, dc, P_(dpooled), P_(idx), B, S, D, P_(dh), 0)
+        # the gradient in h's dtype (autograd would otherwise cast the whole [B, S, D] tensor)
+        dpooled = dpooled.to(ctx.hdtype)
+        dh = torch.zeros(B, S, D, dtype=ctx.hdtype, device=dev)
+        call("clipmi_scatter_rows", s, dcode(ctx.hdtype), P_(dpooled), P_(idx), B, S, D, P_(dh), 0)
         ctx.save = None
         return dh, None, None, None, None
 
@@ -644,19 +671,20 @@ class PoolRowsFn(torch.autograd.Function):
     def forward(ctx, h, runtime, idx):
         dtype = runtime.dtype
         B, S, D = h.shape
-        hc = h.to(dtype).contiguous()
-        out = torch.empty(B, 1, D, dtype=dtype, device=h.device)
-        call("clipmi_gather_rows", K.stream(), dcode(dtype), P_(hc), P_(idx), B, S, D, P_(out))
-        ctx.rt, ctx.idx, ctx.shape = runtime, idx, (B, S, D)
-        return out
+        hd = h.dtype if h.dtype in (torch.float32, torch.bfloat16) else dtype  # gathered in h's own dtype
+        hc = h.to(hd).contiguous()
+        out = torch.empty(B, 1, D, dtype=hd, device=h.device)
+        call("clipmi_gather_rows", K.stream(), dcode(hd), P_(hc), P_(idx), B, S, D, P_(out))
+        ctx.rt, ctx.idx, ctx.shape, ctx.hdtype = runtime, idx, (B, S, D), hd
+        return out.to(dtype)
 
     @staticmethod
     def backward(ctx, dout):
-        dtype = ctx.rt.dtype
+        hd = ctx.hdtype
         B, S, D = ctx.shape
-        d = dout.to(dtype).contiguous()
-        dh = torch.zeros(B, S, D, dtype=dtype, device=dout.device)
-        call("clipmi_scatter_rows", K.stream(), dcode(dtype), P_(d), P_(ctx.idx), B, S, D, P_(dh), 0)
+        d = dout.to(hd).contiguous()
+        dh = torch.zeros(B, S, D, dtype=hd, device=dout.device)
+        call("clipmi_scatter_rows", K.stream(), dcode(hd), P_(d), P_(ctx.idx), B, S, D, P_(dh), 0)
         return dh, None, None
 
 

@@ -24,6 +24,11 @@
 extern "C" {
 int clipmi_layernorm_fwd(void*, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int, int,
                          float, const void*, const void*, int);
+int clipmi_layernorm_fwd2(void*, int, int, void*, int64_t, void*, int64_t, const void*, const void*, float*, float*, int,
+                          int, float, const void*, const void*, int);
+int clipmi_layernorm_bwd2(void*, int, int, const void*, int64_t, const void*, int64_t, const float*, const float*,
+                          const void*, void*, int64_t, const void*, int64_t, float*, float*, int, void*, int64_t, int,
+                          int);
 int64_t clipmi_layernorm_bwd_ws(int R, int D);
 int clipmi_layernorm_bwd(void*, int, const void*, int64_t, const void*, int64_t, const float*, const float*, const void*,
                          void*, int64_t, const void*, int64_t, float*, float*, int, void*, int64_t, int, int);
@@ -211,23 +216,25 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
     }
     return CLIPMI_OK;
   }
+  // the residual stream's dtype: fp32 in the bf16 mode with resid_f32 (x_in, h, x_out), else dt
+  const int xdt = (dt == CLIPMI_BF16 && d->resid_f32) ? CLIPMI_F32 : dt;
   for (int l = 0; l < d->L; ++l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
     void* x_out = (l + 1 < d->L) ? d->act[l + 1].x_in : d->x_out;
-    CLIPMI_TRY(clipmi_layernorm_fwd(s, dt, a.x_in, D, a.ln1, D, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps,
-                                    nullptr, nullptr, 0));
+    CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.x_in, D, a.ln1, D, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps,
+                                     nullptr, nullptr, 0));
     CLIPMI_TRY(gemm(s, dt, R, 3 * D, D, a.ln1, D, true, w.qkv_w, D, true, a.qkv, 3 * D, dt, CLIPMI_EPI_BIAS, w.qkv_b));
     CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
-    CLIPMI_TRY(gemm(s, dt, R, D, D, a.o, D, true, w.out_w, D, true, a.h, D, dt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
+    CLIPMI_TRY(gemm(s, dt, R, D, D, a.o, D, true, w.out_w, D, true, a.h, D, xdt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
                     w.out_b, a.x_in, D));
-    CLIPMI_TRY(clipmi_layernorm_fwd(s, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
-                                    nullptr, nullptr, 0));
+    CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
+                                     nullptr, nullptr, 0));
     // training: a.pre receives quick_gelu'(pre) (computed beside the activation from the fp32
     // pre-activation), so fc2's input gradient below is one product per element
     const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_DACT : 0);
     CLIPMI_TRY(gemm(s, dt, R, F, D, a.ln2, D, true, w.fc1_w, D, true, a.act, F, dt, f1, w.fc1_b, nullptr, 0, a.pre, F));
-    CLIPMI_TRY(gemm(s, dt, R, D, F, a.act, F, true, w.fc2_w, F, true, x_out, D, dt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
+    CLIPMI_TRY(gemm(s, dt, R, D, F, a.act, F, true, w.fc2_w, F, true, x_out, D, xdt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
                     w.fc2_b, a.h, D));
   }
   return CLIPMI_OK;
@@ -248,6 +255,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   CLIPMI_REQUIRE(0 <= layer_lo && layer_lo <= layer_hi && layer_hi <= d->L, "layer range");
   CLIPMI_REQUIRE(d->grads, "encoder_bwd needs gradient destinations");
   const int dt = d->dtype;
+  const int xdt = (dt == CLIPMI_BF16 && d->resid_f32) ? CLIPMI_F32 : dt;  // the saved x_in / h
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
   const WsPlan p = plan(d);
@@ -285,8 +293,8 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w, g.fc2_b));            // gW2 += dx^T act, gb2 += sum dx
     CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w, g.fc1_b));          // gW1 += d_pre^T ln2
     CLIPMI_TRY(gemm(s, dt, R, D, F, dbig, F, true, w.fc1_w, D, false, dln, D, dt, 0));  // d_ln2 = d_pre W1
-    CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx, D, g.ln2_w, g.ln2_b,
-                                    1, wln, ln_bytes, R, D));              // dh = dx + LN2'(d_ln2)
+    CLIPMI_TRY(clipmi_layernorm_bwd2(s, xdt, dt, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx, D, g.ln2_w,
+                                     g.ln2_b, 1, wln, ln_bytes, R, D));   // dh = dx + LN2'(d_ln2)
     // attention branch: g2 is dL/dh
     CLIPMI_TRY(gemm(s, dt, R, D, D, g2, D, true, w.out_w, D, false, dln, D, dt, 0));     // d_o = dh Wo
     CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w, g.out_b));                            // gWo += dh^T o
@@ -294,8 +302,8 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
                                     d->N, D));                              // d_qkv
     CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w, g.qkv_b));  // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
-    CLIPMI_TRY(clipmi_layernorm_bwd(s, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
-                                    g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
+    CLIPMI_TRY(clipmi_layernorm_bwd2(s, xdt, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
+                                     g.ln1_b, 1, wln, ln_bytes, R, D));    // dx_in = dh + LN1'(d_ln1)
   }
   return CLIPMI_OK;
 }

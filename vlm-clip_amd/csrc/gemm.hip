@@ -1233,6 +1233,19 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
     const int dm = (p.var == 32 || w4_pf) ? 102 : (p.var == 28 || w4_default) ? 100 : p.var >= 22 ? 21 - p.var : 1;
     if (const char* l = dispatch_w4(q, s, sel == 3, flags, dm)) return l;
   }
+  // fp32 output of a bf16 product (the bf16 mode's fp32 residual stream: out-projection and fc2 with the
+  // residual fused; the patch embedding; the bf16x3 split products): the same kernels, fp32 epilogue
+  if (f32o && !p.ws && splits == 1 && sel == 3) {
+    if ((w4_default || p.var == 28) && (flags == E_B || flags == (E_B | E_R) || flags == 0)) {
+      if (const char* l = dispatch_w4_f32(p, s, flags)) return l;
+    }
+    switch (flags) {
+      case E_B: launch256<true, true, float, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias_f32";
+      case E_B | E_R: launch256<true, true, float, E_B | E_R, false>(p, splits, s, bg); return "gemm256_fwd_bias_resid_f32";
+      case 0: launch256<true, true, float, 0, false>(p, splits, s, bg); return "gemm256_fwd_f32";
+      default: break;
+    }
+  }
   if (sel == 3 && !f32o) {
     switch (flags) {
       case E_B: launch256<true, true, bf16, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias";

@@ -873,6 +873,18 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
   }
 }
 
+// fp32-output forward products (k-major B) on the persistent kernel: the bf16 mode's fp32 residual stream
+// (fc2 with bias + residual) and fp32-output bf16 products
+const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags) {
+  constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID;
+  switch (flags) {
+    case E_B | E_R: launch_w4p<true, true, float, E_B | E_R, false>(p, 1, s, nullptr); return "gemm256_fwd_bias_resid_f32";
+    case E_B: launch_w4p<true, true, float, E_B, false>(p, 1, s, nullptr); return "gemm256_fwd_bias_f32";
+    case 0: launch_w4p<true, true, float, 0, false>(p, 1, s, nullptr); return "gemm256_fwd_f32";
+    default: return nullptr;
+  }
+}
+
 // weight gradients (both operands row-major in k, fp32 output): split-K slabs (p.ws) or the
 // beta epilogue (one split), with the fused bias gradient when bg != nullptr
 // MXFP8 forward products on the persistent 4-wave kernel: K % 256 == 0 (whole scale pairs) and at

@@ -51,10 +51,10 @@ constexpr int LN_RPW = 2;
 // Q8: y is written as MXFP8 instead (q8 [R, D] e4m3 bytes, s8 [R, D/32] E8M0): a 32-element
 // block is 8 consecutive lanes' 4-element pieces (PS == 4), max-reduced across those lanes; the
 // fp8 operand of the next GEMM without a bf16 round trip through HBM.
-template <typename T, int PS, int NP, bool Q8 = false>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
+template <typename TX, typename T, int PS, int NP, bool Q8 = false>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(TX* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
                                                      float* mean_out, float* rstd_out, int R, int D, float eps,
-                                                     const T* pos, const T* cls, int period, uint8_t* q8 = nullptr,
+                                                     const TX* pos, const TX* cls, int period, uint8_t* q8 = nullptr,
                                                      uint8_t* s8 = nullptr) {
   static_assert(!Q8 || PS == 4, "MXFP8 output needs 4-element pieces");
   const int lane = threadIdx.x & 63;
@@ -64,9 +64,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, in
 #pragma unroll
   for (int rr = 0; rr < LN_RPW; ++rr) {
     const int row = min(row0 + rr, R - 1);  // a tail wave recomputes row R-1 and does not store it twice
-    T* xr = x + (int64_t)row * ldx;
+    TX* xr = x + (int64_t)row * ldx;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) vload<T, PS>(xr + (k * 64 + lane) * PS, v[rr][k]);
+    for (int k = 0; k < NP; ++k) vload<TX, PS>(xr + (k * 64 + lane) * PS, v[rr][k]);
   }
   float mean[LN_RPW], rstd[LN_RPW];
 #pragma unroll
@@ -80,15 +80,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, in
       if (pos) {
         const int t = row % period;
         float pv[PS];
-        vload<T, PS>(pos + (int64_t)t * D + c, pv);
+        vload<TX, PS>(pos + (int64_t)t * D + c, pv);
 #pragma unroll
         for (int j = 0; j < PS; ++j) v[rr][k][j] += pv[j];
         if (cls && t == 0) {
-          vload<T, PS>(cls + c, pv);
+          vload<TX, PS>(cls + c, pv);
 #pragma unroll
           for (int j = 0; j < PS; ++j) v[rr][k][j] += pv[j];
         }
-        if (own) vstore<T, PS>(x + (int64_t)row * ldx + c, v[rr][k]);
+        if (own) vstore<TX, PS>(x + (int64_t)row * ldx + c, v[rr][k]);
       }
 #pragma unroll
       for (int j = 0; j < PS; ++j) s += v[rr][k][j];
@@ -140,8 +140,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(T* x, int64_t ldx, T* y, in
 
 // dx = [dres +] rstd * (g - mean(g) - xhat * mean(g*xhat)),  g = dy * w
 // per-block partial dgamma/dbeta -> ws[blockIdx][2][D]
-template <typename T, int PS, int NP>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, const T* x, int64_t ldx,
+template <typename TX, typename T, int PS, int NP>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, const TX* x, int64_t ldx,
                                                      const float* mean, const float* rstd, const T* w,
                                                      T* dx, int64_t lddx, const T* dres, int64_t ldres,
                                                      float* ws, int R, int D) {
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
         const int c = (k * 64 + lane) * PS;
         if (dres) vload<T, PS>(dres + (int64_t)row * ldres + c, rr[q][k]);
         vload<T, PS>(dy + (int64_t)row * lddy + c, d[q][k]);
-        vload<T, PS>(x + (int64_t)row * ldx + c, xh[q][k]);
+        vload<TX, PS>(x + (int64_t)row * ldx + c, xh[q][k]);
       }
     }
 #pragma unroll
@@ -231,14 +231,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
 // one wave per row, three passes over the row (sum, centred sum of squares, normalise), the row
 // re-read from the cache.  For the modules whose width is free (peclip ContextAdapter / SharedAdapter,
 // nn.MultiheadAttention accepts any embed_dim divisible by num_heads; the adapters' LayerNorm).
-template <typename T>
-__global__ __launch_bounds__(256) void ln_fwd_any_kernel(T* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
+template <typename TX, typename T>
+__global__ __launch_bounds__(256) void ln_fwd_any_kernel(TX* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
                                                          float* mean_out, float* rstd_out, int R, int D, float eps,
-                                                         const T* pos, const T* cls, int period) {
+                                                         const TX* pos, const TX* cls, int period) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
-  T* xr = x + (int64_t)row * ldx;
+  TX* xr = x + (int64_t)row * ldx;
   const int t = pos ? row % period : 0;
   float s = 0.f;
   for (int c = lane; c < D; c += 64) {
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void ln_fwd_any_kernel(T* x, int64_t ldx, T* y
     if (pos) {
       v += (float)pos[(int64_t)t * D + c];
       if (cls && t == 0) v += (float)cls[c];
-      xr[c] = (T)v;
+      xr[c] = (TX)v;
       v = (float)xr[c];  // the stored (rounded) sum, as the register kernels normalise it
     }
     s += v;
@@ -268,8 +268,8 @@ __global__ __launch_bounds__(256) void ln_fwd_any_kernel(T* x, int64_t ldx, T* y
 
 // dx = [dres +] rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partial dgamma /
 // dbeta -> ws[blockIdx][2][D] (each wave's own LDS row pair, summed in wave order: deterministic)
-template <typename T>
-__global__ __launch_bounds__(256) void ln_bwd_any_kernel(const T* dy, int64_t lddy, const T* x, int64_t ldx,
+template <typename TX, typename T>
+__global__ __launch_bounds__(256) void ln_bwd_any_kernel(const T* dy, int64_t lddy, const TX* x, int64_t ldx,
                                                          const float* mean, const float* rstd, const T* w, T* dx,
                                                          int64_t lddx, const T* dres, int64_t ldres, float* ws, int R,
                                                          int D) {
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void ln_bwd_any_kernel(const T* dy, int64_t ld
   for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
     const T* dyr = dy + (int64_t)row * lddy;
-    const T* xr = x + (int64_t)row * ldx;
+    const TX* xr = x + (int64_t)row * ldx;
     float s1 = 0.f, s2 = 0.f;
     for (int c = lane; c < D; c += 64) {
       const float g = (float)dyr[c] * (float)w[c];
@@ -582,39 +582,39 @@ __global__ __launch_bounds__(256) void id_chunk_sum_kernel(const int* perm, cons
   }
 }
 
-template <typename T, int PS, int NP>
+template <typename TX, typename T, int PS, int NP>
 void ln_fwd_launch(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, const void* w, const void* b,
                    float* mean, float* rstd, int R, int D, float eps, const void* pos, const void* cls, int period) {
-  hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s, (T*)x, ldx, (T*)y, ldy,
-                     (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const T*)pos, (const T*)cls, period);
+  hipLaunchKernelGGL((ln_fwd_kernel<TX, T, PS, NP>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s, (TX*)x, ldx,
+                     (T*)y, ldy, (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const TX*)pos, (const TX*)cls, period);
 }
-template <typename T, int PS, int NP>
+template <typename TX, typename T, int PS, int NP>
 void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t* s8, const void* w, const void* b,
                       float* mean, float* rstd, int R, int D, float eps) {
   if constexpr (PS == 4) {
-    hipLaunchKernelGGL((ln_fwd_kernel<T, PS, NP, true>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s,
-                       (T*)x, ldx, (T*)nullptr, (int64_t)0, (const T*)w, (const T*)b, mean, rstd, R, D, eps,
-                       (const T*)nullptr, (const T*)nullptr, 1, q8, s8);
+    hipLaunchKernelGGL((ln_fwd_kernel<TX, T, PS, NP, true>), dim3((R + 4 * LN_RPW - 1) / (4 * LN_RPW)), dim3(256), 0, s,
+                       (TX*)x, ldx, (T*)nullptr, (int64_t)0, (const T*)w, (const T*)b, mean, rstd, R, D, eps,
+                       (const TX*)nullptr, (const TX*)nullptr, 1, q8, s8);
   }
 }
 // grid (in: the partial-sum rows the workspace holds; out: the blocks launched = partial rows
 // written): at most the blocks the CUs hold at once, so no block starts a second round late
 // (the D = 768 form keeps two rows' loads in registers: 164 VGPRs, 3 waves per SIMD)
-template <typename T, int PS, int NP>
+template <typename TX, typename T, int PS, int NP>
 void ln_bwd_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                    int64_t ldres, float* ws, int R, int D) {
   static int resident = [] {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<T, PS, NP>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<TX, T, PS, NP>, 256, 0) !=
             hipSuccess || per_cu < 1)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     return per_cu * cus;
   }();
   if (grid > resident) grid = resident;
-  hipLaunchKernelGGL((ln_bwd_kernel<T, PS, NP>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const T*)x, ldx,
+  hipLaunchKernelGGL((ln_bwd_kernel<TX, T, PS, NP>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const TX*)x, ldx,
                      mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
 }
 
@@ -626,45 +626,62 @@ inline bool ln_fast_width(int D) {
 }
 
 // dispatch on (PS, NP) from D
-#define LN_DISPATCH(D, FN, T, ...)                                              \
+// (TX: the normalised input x; T: everything else -- output / gradients / affine weights)
+#define LN_DISPATCH(D, FN, TX, T, ...)                                          \
   do {                                                                          \
     const int q_ = (D) / 64;                                                    \
-    if (q_ == 16) FN<T, 4, 4>(__VA_ARGS__);                                     \
-    else if (q_ == 12) FN<T, 4, 3>(__VA_ARGS__);                                \
-    else if (q_ == 8) FN<T, 4, 2>(__VA_ARGS__);                                 \
-    else if (q_ == 4) FN<T, 4, 1>(__VA_ARGS__);                                 \
-    else if (q_ == 2) FN<T, 2, 1>(__VA_ARGS__);                                 \
-    else if (q_ == 1) FN<T, 1, 1>(__VA_ARGS__);                                 \
-    else if (q_ == 6) FN<T, 2, 3>(__VA_ARGS__);                                 \
-    else if (q_ == 3) FN<T, 1, 3>(__VA_ARGS__);                                 \
+    if (q_ == 16) FN<TX, T, 4, 4>(__VA_ARGS__);                                 \
+    else if (q_ == 12) FN<TX, T, 4, 3>(__VA_ARGS__);                            \
+    else if (q_ == 8) FN<TX, T, 4, 2>(__VA_ARGS__);                             \
+    else if (q_ == 4) FN<TX, T, 4, 1>(__VA_ARGS__);                             \
+    else if (q_ == 2) FN<TX, T, 2, 1>(__VA_ARGS__);                             \
+    else if (q_ == 1) FN<TX, T, 1, 1>(__VA_ARGS__);                             \
+    else if (q_ == 6) FN<TX, T, 2, 3>(__VA_ARGS__);                             \
+    else if (q_ == 3) FN<TX, T, 1, 3>(__VA_ARGS__);                             \
     else return clipmi_invalid("layernorm: unsupported hidden size");           \
   } while (0)
 
 }  // namespace
 
 // ------------------------------------------------------------------------- C ABI
-extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy,
-                                    const void* w, const void* b, float* mean, float* rstd, int R, int D,
-                                    float eps, const void* pos, const void* cls, int period) {
+// x_dtype: the normalised input's dtype; dtype: the output's, the affine weights' and (backward) the
+// gradients'.  Combinations: equal dtypes, or fp32 x with bf16 everything else (the bf16 mode's fp32
+// residual stream feeding bf16 GEMM operands).
+static int ln_types_ok(int x_dtype, int dtype) {
+  return (dtype == CLIPMI_BF16 || dtype == CLIPMI_F32) && (x_dtype == dtype || (x_dtype == CLIPMI_F32 && dtype == CLIPMI_BF16));
+}
+
+template <typename TX, typename T>
+static int ln_fwd_t(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, const void* w, const void* b, float* mean,
+                    float* rstd, int R, int D, float eps, const void* pos, const void* cls, int period) {
+  if (!ln_fast_width(D)) {  // any other width: the one-wave-per-row kernel
+    hipLaunchKernelGGL((ln_fwd_any_kernel<TX, T>), dim3((R + 3) / 4), dim3(256), 0, s, (TX*)x, ldx, (T*)y, ldy,
+                       (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const TX*)pos, (const TX*)cls, period);
+    return CLIPMI_OK;
+  }
+  LN_DISPATCH(D, ln_fwd_launch, TX, T, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+  return CLIPMI_OK;
+}
+
+extern "C" int clipmi_layernorm_fwd2(void* stream, int x_dtype, int dtype, void* x, int64_t ldx, void* y, int64_t ldy,
+                                     const void* w, const void* b, float* mean, float* rstd, int R, int D, float eps,
+                                     const void* pos, const void* cls, int period) {
   hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(ln_types_ok(x_dtype, dtype), "layernorm: dtypes (equal, or fp32 x with bf16 y)");
   CLIPMI_REQUIRE(D >= 1 && D <= LN_ANY_MAX_D, "D must be in [1, 4096]");
   CLIPMI_REQUIRE(!pos || period > 0, "period");
   if (R == 0) return CLIPMI_OK;
-  if (!ln_fast_width(D)) {  // any other width: the one-wave-per-row kernel
-    const dim3 g((R + 3) / 4);
-    if (dtype == CLIPMI_BF16)
-      hipLaunchKernelGGL(ln_fwd_any_kernel<bf16>, g, dim3(256), 0, s, (bf16*)x, ldx, (bf16*)y, ldy, (const bf16*)w,
-                         (const bf16*)b, mean, rstd, R, D, eps, (const bf16*)pos, (const bf16*)cls, period);
-    else
-      hipLaunchKernelGGL(ln_fwd_any_kernel<float>, g, dim3(256), 0, s, (float*)x, ldx, (float*)y, ldy, (const float*)w,
-                         (const float*)b, mean, rstd, R, D, eps, (const float*)pos, (const float*)cls, period);
-    CLIPMI_CHECK_LAUNCH();
-    return CLIPMI_OK;
-  }
-  if (dtype == CLIPMI_BF16) LN_DISPATCH(D, ln_fwd_launch, bf16, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
-  else LN_DISPATCH(D, ln_fwd_launch, float, s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+  if (dtype == CLIPMI_F32) CLIPMI_TRY((ln_fwd_t<float, float>(s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period)));
+  else if (x_dtype == CLIPMI_F32) CLIPMI_TRY((ln_fwd_t<float, bf16>(s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period)));
+  else CLIPMI_TRY((ln_fwd_t<bf16, bf16>(s, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period)));
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
+}
+
+extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ldx, void* y, int64_t ldy,
+                                    const void* w, const void* b, float* mean, float* rstd, int R, int D,
+                                    float eps, const void* pos, const void* cls, int period) {
+  return clipmi_layernorm_fwd2(stream, dtype, dtype, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
 }
 
 extern "C" int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, uint8_t* q8,
@@ -675,7 +692,7 @@ extern "C" int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x
   CLIPMI_REQUIRE(D % 256 == 0 && D <= 1024, "layernorm_fwd_mxfp8: D must be a multiple of 256, <= 1024");
   CLIPMI_REQUIRE(q8 && s8, "layernorm_fwd_mxfp8: outputs");
   if (R == 0) return CLIPMI_OK;
-  LN_DISPATCH(D, ln_fwd_q8_launch, bf16, s, (void*)x, ldx, q8, s8, w, b, mean, rstd, R, D, eps);
+  LN_DISPATCH(D, ln_fwd_q8_launch, bf16, bf16, s, (void*)x, ldx, q8, s8, w, b, mean, rstd, R, D, eps);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
@@ -688,33 +705,45 @@ extern "C" int64_t clipmi_layernorm_bwd_ws(int R, int D) {
   return (int64_t)nb * 2 * D * 4;
 }
 
+template <typename TX, typename T>
+static int ln_bwd_t(hipStream_t s, int& nb, const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* mean,
+                    const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres, int64_t ldres, float* wsf,
+                    int R, int D) {
+  if (!ln_fast_width(D)) {
+    const size_t lds = wsf ? (size_t)4 * 2 * D * 4 : 0;
+    (void)lds_optin((const void*)ln_bwd_any_kernel<TX, T>, (int)lds);
+    hipLaunchKernelGGL((ln_bwd_any_kernel<TX, T>), dim3(nb), dim3(256), lds, s, (const T*)dy, lddy, (const TX*)x, ldx,
+                       mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, wsf, R, D);
+    return CLIPMI_OK;
+  }
+  LN_DISPATCH(D, ln_bwd_launch, TX, T, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  return CLIPMI_OK;
+}
+
 extern "C" int clipmi_layernorm_bwd(void* stream, int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                                     const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx,
                                     const void* dres, int64_t ldres, float* dw, float* db, int beta_wb,
                                     void* ws, int64_t ws_bytes, int R, int D) {
+  return clipmi_layernorm_bwd2(stream, dtype, dtype, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, dw, db,
+                               beta_wb, ws, ws_bytes, R, D);
+}
+
+extern "C" int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const void* dy, int64_t lddy, const void* x,
+                                     int64_t ldx, const float* mean, const float* rstd, const void* w, void* dx,
+                                     int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db, int beta_wb,
+                                     void* ws, int64_t ws_bytes, int R, int D) {
   hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(ln_types_ok(x_dtype, dtype), "layernorm: dtypes (equal, or fp32 x with bf16 gradients)");
   CLIPMI_REQUIRE(D >= 1 && D <= LN_ANY_MAX_D, "D must be in [1, 4096]");
   if (R == 0) return CLIPMI_OK;
   int nb = (R + 3) / 4;
   if (nb > 1024) nb = 1024;
   float* wsf = (dw || db) ? (float*)ws : nullptr;
   if (wsf) CLIPMI_REQUIRE(ws_bytes >= (int64_t)nb * 2 * D * 4, "layernorm_bwd workspace too small");
-  if (!ln_fast_width(D)) {
-    const size_t lds = wsf ? (size_t)4 * 2 * D * 4 : 0;
-    if (dtype == CLIPMI_BF16) {
-      (void)lds_optin((const void*)ln_bwd_any_kernel<bf16>, (int)lds);
-      hipLaunchKernelGGL(ln_bwd_any_kernel<bf16>, dim3(nb), dim3(256), lds, s, (const bf16*)dy, lddy, (const bf16*)x, ldx,
-                         mean, rstd, (const bf16*)w, (bf16*)dx, lddx, (const bf16*)dres, ldres, wsf, R, D);
-    } else {
-      (void)lds_optin((const void*)ln_bwd_any_kernel<float>, (int)lds);
-      hipLaunchKernelGGL(ln_bwd_any_kernel<float>, dim3(nb), dim3(256), lds, s, (const float*)dy, lddy, (const float*)x,
-                         ldx, mean, rstd, (const float*)w, (float*)dx, lddx, (const float*)dres, ldres, wsf, R, D);
-    }
-  } else if (dtype == CLIPMI_BF16) {
-    LN_DISPATCH(D, ln_bwd_launch, bf16, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
-  } else {
-    LN_DISPATCH(D, ln_bwd_launch, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
-  }
+  // the fast kernels shrink nb to the resident block count (the partial rows they write)
+  if (dtype == CLIPMI_F32) CLIPMI_TRY((ln_bwd_t<float, float>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
+  else if (x_dtype == CLIPMI_F32) CLIPMI_TRY((ln_bwd_t<float, bf16>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
+  else CLIPMI_TRY((ln_bwd_t<bf16, bf16>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
   CLIPMI_CHECK_LAUNCH();
   if (((uintptr_t)wsf & 15) != 0 || D % 4 != 0) {
     if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
