@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--model", default="B/16")
     ap.add_argument("--mode", default="full", choices=["full", "adapter"])
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32", "bf16x3"],
                     help="fp8: the frozen towers' GEMMs in MXFP8 (BASELINE config 5; needs --mode adapter); "
                          "fp32: the parity mode (f32 operands end to end), priced against the f32 MFMA peak")
     ap.add_argument("--roofline-family", default=None, choices=list(FAMILIES) + list(FAMILIES_FP32),
@@ -92,7 +92,10 @@ FAMILIES = {
                           "gemm256_fwd_bias_qgelu_dact", "gemm256_fwd_bias_qgelu", "gemm256_fwd", "gemm256_dgrad",
                           "gemm256_dgrad_dqgelu", "gemm256_dgrad_mulaux",
                           # fp32 residual stream: out-projection / fc2 write the fp32 sum (round 5)
-                          "gemm256_fwd_bias_resid_f32", "gemm256_fwd_bias_f32", "gemm256_fwd_f32"],
+                          "gemm256_fwd_bias_resid_f32", "gemm256_fwd_bias_f32", "gemm256_fwd_f32",
+                          # --precision bf16x3: the split products' fp32-output instances
+                          "gemm256_fwd_bias_qgelu_dact_f32", "gemm256_fwd_bias_qgelu_f32", "gemm256_dgrad_f32",
+                          "gemm256_dgrad_mulaux_f32"],
     "gemm256_wgrad": ["gemm256_wgrad_splitk", "gemm256_wgrad"],
     "attention": ["attn_fwd", "attn_bwd"],
     "gemm_fp8": ["gemm_fp8_fwd_bias", "gemm_fp8_fwd_bias_resid", "gemm_fp8_fwd_bias_qgelu",
@@ -256,7 +259,7 @@ def self_launch(args):
     return subprocess.run(cmd, env=env).returncode
 
 
-def family_roofline(name, launches, cfg, B, train, resid32=False):
+def family_roofline(name, launches, cfg, B, train, resid32=False, x3=False):
     """launches: [(ms, flops)] of one family on the caller's stream inside the timed steps."""
     if not launches:
         return None
@@ -264,7 +267,9 @@ def family_roofline(name, launches, cfg, B, train, resid32=False):
     tot_fl = sum(f for _, f in launches)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
     peak = PEAKS.get(name, PEAK_BF16_TFLOPS)
-    alg = algorithmic_bytes(cfg, B, train, resid32).get(name)
+    # bf16x3: the launches are the split products (3K bf16 reduction, fp32 C); their flops are the MFMA
+    # work issued (3x the fp32 product's) and the bf16-operand byte model does not apply
+    alg = None if x3 else algorithmic_bytes(cfg, B, train, resid32).get(name)
     res = {"bound": "mfma", "kernel": name, "labels": {**FAMILIES, **FAMILIES_FP32}[name], "launches": len(launches),
            "avg_launch_ms": round(tot_ms / len(launches), 4), "flops_per_launch": tot_fl / len(launches),
            "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
@@ -403,7 +408,7 @@ def main():
     roofs = {}
     for name in fams:
         r = family_roofline(name, per_fam[name], cfg, args.batch, not adapters,
-                            resid32=bool(getattr(model._rt, "resid32", False)))
+                            resid32=bool(getattr(model._rt, "resid32", False)), x3=args.precision == "bf16x3")
         if r is not None:
             r["ms_per_step_caller_stream"] = round(sum(m for m, _ in per_fam[name]) / args.steps, 2)
             roofs[name] = r
@@ -416,7 +421,8 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": {"fp8": "fp8 (MXFP8 e4m3 tower GEMMs; bf16 elsewhere)", "fp32": "fp32"}.get(args.precision, "bf16"),
+        "dtype": {"fp8": "fp8 (MXFP8 e4m3 tower GEMMs; bf16 elsewhere)", "fp32": "fp32",
+                  "bf16x3": "fp32 (tower GEMMs as bf16x3 split products, fp32 accumulation)"}.get(args.precision, "bf16"),
         "data": f"synthetic: CLIP-normalised U[0,1) {cfg.vision_config.image_size}px pixels + BOS/random-id/EOS captions (77 tok, EOS pad), "
                 "random-init weights",
         "config": {"workload": f"{cfg.name} {'full fine-tune (adapters off)' if not adapters else 'adapter fine-tune'}"
@@ -424,7 +430,9 @@ def main():
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": cfg.vision_config.image_size,
                    "text_len": 77, "parallelism": f"dp{world}"},
-        "mfma_frac_step": round(value * step_flops_pair / (world * {"fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_FP32_TFLOPS}
+        # bf16x3: the model's flops against a third of the bf16 peak (three bf16 products per fp32 one)
+        "mfma_frac_step": round(value * step_flops_pair / (world * {"fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_FP32_TFLOPS,
+                                                                    "bf16x3": PEAK_BF16_TFLOPS / 3}
                                                            .get(args.precision, PEAK_BF16_TFLOPS) * 1e12), 4),
         "step_tflops_per_gpu": round(value * step_flops_pair / world / 1e12, 1),
         "loss": round(float(loss.item()), 4),

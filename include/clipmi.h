@@ -93,6 +93,15 @@ typedef struct clipmi_gemm_desc {
 /* C *= aux[m,n] (the stored derivative: d_pre = d_act * act'(pre)) */
 #define CLIPMI_EPI_MUL_AUX 512
 
+/* Not an epilogue: ab_dtype and c_dtype CLIPMI_F32, computed on the bf16 MFMA kernels as a split-operand
+ * product (precision "bf16x3"): x = bf16(x) + bf16(x - bf16(x)) for both operands and
+ * A.B^T ~ Ah.Bh^T + Ah.Bl^T + Al.Bh^T in one bf16 GEMM over 3K (fp32 accumulation), ~2^-16 relative
+ * error per product instead of bf16's 2^-8.  Any epilogue flag except bias_grad; K % 8 == 0 when an operand
+ * is k-major (the bf16 kernels' layout rules apply to the split images: row-major A needs M % 8 == 0); workspace
+ * >= clipmi_gemm_split3_ws(...) bytes, 256-byte aligned (it also holds the split-K slabs). */
+#define CLIPMI_GEMM_SPLIT3 1024
+int64_t clipmi_gemm_split3_ws(int M, int N, int K, int a_kmajor, int b_kmajor, int split_k);
+
 int clipmi_gemm(void* stream, const clipmi_gemm_desc* d);
 /* Strided batch of nb1 x nb2 fp32 products (exact f32; flags: beta only): product z = i1 * nb2 + i2 reads
  * A + i1 * sa1 + i2 * sa2, B + i1 * sb1 + i2 * sb2 and writes C + i1 * sc1 + i2 * sc2 (elements), the
@@ -252,9 +261,18 @@ typedef struct clipmi_encoder_desc {
    * operand stays bf16.  The reference is fp32 end to end (trainer.py:81-99); rounding the residual sum
    * to bf16 at each of the 2L residual adds was the largest bf16-mode error (profiles/r05_bf16_error_sources.log). */
   int resid_f32;
+  /* dtype CLIPMI_F32 only (precision "bf16x3"): every GEMM of the forward and backward runs as a
+   * split-operand bf16 product (CLIPMI_GEMM_SPLIT3) with its split images in x3_ws (x3_ws_bytes >=
+   * clipmi_encoder_x3_ws, 256-byte aligned; one scratch per concurrently running encoder); activations,
+   * LayerNorm, attention and gradients stay fp32. */
+  int gemm_x3;
+  void* x3_ws;
+  int64_t x3_ws_bytes;
 } clipmi_encoder_desc;
 int clipmi_encoder_fwd(void* stream, const clipmi_encoder_desc* d);
 int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d);
+/* the split-image scratch of a gemm_x3 encoder (forward and backward; 0 when gemm_x3 is off) */
+int64_t clipmi_encoder_x3_ws(const clipmi_encoder_desc* d);
 /* dx: dL/d(encoder output) in, dL/d(encoder input) out */
 int clipmi_encoder_bwd(void* stream, const clipmi_encoder_desc* d, void* dx);
 /* the same for layers layer_hi-1 .. layer_lo only (chunked backward: each chunk's gradient slice

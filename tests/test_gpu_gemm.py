@@ -336,3 +336,57 @@ def test_gemm_raster_groups_bitwise(raster, var, monkeypatch):
         outs.append(C)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+# ---- bf16x3 split-operand fp32 GEMM (CLIPMI_GEMM_SPLIT3, precision "bf16x3")
+@pytest.mark.parametrize("akm,bkm,flags,split", [
+    (True, True, 0, 1), (True, True, _lib.EPI_BIAS, 1), (True, True, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    (True, True, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT, 1), (True, True, _lib.EPI_BIAS | _lib.EPI_QGELU, 1),
+    (True, False, 0, 1), (True, False, _lib.EPI_MUL_AUX, 1),
+    (False, False, _lib.EPI_BETA, 1), (False, False, _lib.EPI_BETA, 5), (False, True, 0, 1)])
+@pytest.mark.parametrize("M,N,K", [(1000, 776, 768), (520, 384, 3072), (77, 64, 128), (2048, 256, 512)])
+def test_gemm_split3_fp32_accuracy(akm, bkm, flags, split, M, N, K):
+    """fp32 operands through the bf16x3 split product: against an fp64 reference the error is ~2^-16
+    relative per product (the dropped lo x lo term plus fp32 accumulation), 30x+ below a plain bf16
+    product of the same operands, on every layout / epilogue the bf16x3 mode issues."""
+    if not akm and M % 8:
+        pytest.skip("row-major A needs M % 8 == 0")
+    A = _mk((M, K) if akm else (K, M), torch.float32, 1)
+    B = _mk((N, K) if bkm else (K, N), torch.float32, 2)
+    Ad = (A if akm else A.t()).double()
+    Bd = (B if bkm else B.t()).double()
+    acc = Ad @ Bd.t()
+    bias, res, aux = _mk((N,), torch.float32, 3), _mk((M, N), torch.float32, 4), None
+    cold = _mk((M, N), torch.float32, 5)
+    if flags & _lib.EPI_MUL_AUX:
+        aux = _mk((M, N), torch.float32, 6)
+    elif flags & _lib.EPI_STORE_DACT:
+        aux = torch.zeros(M, N, device="cuda")
+    C = cold.clone() if flags & _lib.EPI_BETA else torch.empty(M, N, device="cuda")
+    kern.gemm(M, N, K, A, K if akm else M, akm, B, K if bkm else N, bkm, C, N, bias=bias if flags & _lib.EPI_BIAS else None,
+              residual=res if flags & _lib.EPI_RESID else None, ldr=N if flags & _lib.EPI_RESID else 0,
+              aux=aux, ldaux=N if aux is not None else 0, flags=flags, split_k=split, split3=True)
+    ref, pre = _ref_epi(acc, flags, bias.double(), None if aux is None else aux.double(), res.double(),
+                        cold.double())
+    scale = acc.abs().max().item()
+    err = (C.double() - ref).abs().max().item() / scale
+    # the same product with bf16-rounded operands: the precision bf16x3 buys back
+    e16 = (((A.bfloat16().double() if akm else A.t().bfloat16().double()) @
+            (B.bfloat16().double() if bkm else B.t().bfloat16().double()).t()) - acc).abs().max().item() / scale
+    assert err < 2e-5 and err * 30 < e16, (err, e16)
+    if flags & _lib.EPI_STORE_DACT:
+        # quick_gelu'(v) at the computed pre-activation: v carries err * scale absolute error (scale ~ 130
+        # here) and |quick_gelu''| < 1, plus the kernel's fast exp: measured 3.8e-4
+        assert ((aux.double() - pre).abs().max().item()) < 2e-3
+
+
+def test_gemm_split3_rejects_bad_workspace_and_bias_grad():
+    A, B = _mk((256, 256), torch.float32, 1), _mk((256, 256), torch.float32, 2)
+    C = torch.empty(256, 256, device="cuda")
+    with pytest.raises(ValueError, match="split3"):
+        kern.gemm(256, 256, 256, A, 256, False, B, 256, False, C, 256, flags=_lib.EPI_BETA,
+                  bias_grad=torch.zeros(256, device="cuda"), split3=True)
+    with pytest.raises(ValueError, match="workspace"):
+        kern.gemm(256, 256, 256, A, 256, True, B, 256, True, C, 256, flags=_lib.GEMM_SPLIT3,
+                  workspace=torch.empty(1024, dtype=torch.uint8, device="cuda"))
+

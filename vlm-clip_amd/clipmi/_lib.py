@@ -15,6 +15,7 @@ F32, BF16, FP8 = 0, 1, 2
 EPI_BIAS, EPI_QGELU, EPI_GELU, EPI_RESID = 1, 2, 4, 8
 EPI_DQGELU, EPI_DGELU, EPI_BETA, EPI_STORE_PRE = 16, 32, 64, 128
 EPI_STORE_DACT, EPI_MUL_AUX = 256, 512
+GEMM_SPLIT3 = 1024  # not an epilogue: fp32 operands as a bf16x3 split product (include/clipmi.h)
 
 c_i64 = ctypes.c_int64
 c_vp = ctypes.c_void_p
@@ -53,6 +54,7 @@ _declare("clipmi_version", ctypes.c_int, [])
 _declare("clipmi_build_digest", ctypes.c_char_p, [])
 _declare("clipmi_last_error", ctypes.c_char_p, [])
 _declare("clipmi_gemm", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc)])
+_declare("clipmi_gemm_split3_ws", ctypes.c_int64, [ctypes.c_int] * 6)
 _declare("clipmi_gemm_batched", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc), ctypes.c_int, ctypes.c_int]
          + [ctypes.c_int64] * 6)
 

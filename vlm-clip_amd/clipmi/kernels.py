@@ -37,11 +37,18 @@ def _on_gpu(*ts):
 
 
 def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, residual=None, ldr=0,
-         aux=None, ldaux=0, alpha=1.0, flags=0, split_k=1, workspace=None, bias_grad=None, small_tile=False):
-    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see include/clipmi.h clipmi_gemm."""
+         aux=None, ldaux=0, alpha=1.0, flags=0, split_k=1, workspace=None, bias_grad=None, small_tile=False,
+         split3=False):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see include/clipmi.h clipmi_gemm.  split3: fp32 operands
+    and output computed as a bf16x3 split product on the bf16 MFMA kernels (CLIPMI_GEMM_SPLIT3; its
+    split images and any split-K slabs in a scratch allocated here, `workspace` is not used)."""
     _on_gpu(A, B, C, bias, residual, aux, workspace)
     if A.dtype != B.dtype:
         raise ValueError("A and B must share a dtype")
+    if split3:
+        flags |= _lib.GEMM_SPLIT3
+        nb = int(_lib.lib().clipmi_gemm_split3_ws(M, N, K, int(a_kmajor), int(b_kmajor), split_k))
+        workspace = torch.empty(max(nb, 16), dtype=torch.uint8, device=C.device)
     d = GemmDesc()
     d.M, d.N, d.K = M, N, K
     d.A, d.lda, d.a_kmajor = A.data_ptr(), lda, int(a_kmajor)

@@ -5,8 +5,10 @@ checkpoint format and error types as the reference; the compute runs on libclipm
 (``clipmi.towers``).  Extensions, all keyword-only:
 
   device       where the fp32 parameter arenas live (default: cuda if available)
-  precision    "bf16" (MFMA path, default), "fp32" (exact-f32 parity mode) or "fp8" (frozen towers
-               with MXFP8 GEMMs, BASELINE config 5; adapters and the loss stay bf16 / fp32)
+  precision    "bf16" (MFMA path, default; fp32 residual stream), "fp32" (exact-f32 parity mode),
+               "bf16x3" (fp32 activations with the towers' GEMMs as bf16x3 split products on the MFMA
+               kernels: north_star's 1e-3 logits at several times the fp32 mode's speed) or "fp8" (frozen
+               towers with MXFP8 GEMMs, BASELINE config 5; adapters and the loss stay bf16 / fp32)
   pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
                (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
   init_seed    seed of the deterministic random init used when no weights file exists
@@ -80,8 +82,8 @@ class CLIPWithAdapters(nn.Module):
         super().__init__()
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
-        if precision not in ("bf16", "fp32", "fp8"):
-            raise ValueError("precision must be 'bf16', 'fp32' or 'fp8'")
+        if precision not in ("bf16", "fp32", "bf16x3", "fp8"):
+            raise ValueError("precision must be 'bf16', 'fp32', 'bf16x3' or 'fp8'")
         if precision == "fp8" and not freeze_clip:
             raise ValueError("precision='fp8' runs the frozen towers only (MXFP8 forward GEMMs); use freeze_clip=True")
         if pooling not in ("first", "eos"):
@@ -91,8 +93,9 @@ class CLIPWithAdapters(nn.Module):
         self.precision = precision
         self.pooling = pooling
         self.process_group = process_group
-        dtype = torch.float32 if precision == "fp32" else torch.bfloat16
-        shadow = precision != "fp32"
+        exact = precision in ("fp32", "bf16x3")  # fp32 activations and weights (no bf16 shadow)
+        dtype = torch.float32 if exact else torch.bfloat16
+        shadow = not exact
         # model_m.py:29-30 — CLIPModel.from_pretrained / CLIPProcessor.from_pretrained
         self.clip = CLIPParams(cfg, device, shadow)
         self.clip.text_model.config = cfg.text_config
@@ -126,6 +129,8 @@ class CLIPWithAdapters(nn.Module):
         self._rt.fp8 = precision == "fp8"
         # bf16 mode: the towers' residual stream in fp32 (engine resid_f32; profiles/r05_bf16_error_sources.log)
         self._rt.resid32 = precision == "bf16"
+        # bf16x3: the towers' GEMMs (patch embedding, every encoder GEMM) as split-operand bf16 products
+        self._rt.x3 = precision == "bf16x3"
         if freeze_clip:
             self._freeze_clip_parameters()
 

@@ -58,13 +58,14 @@ class EncoderDesc(ctypes.Structure):
                 ("layers", ctypes.POINTER(LayerW)), ("grads", ctypes.POINTER(LayerG)),
                 ("act", ctypes.POINTER(LayerAct)), ("x_out", c_vp), ("workspace", c_vp),
                 ("workspace_bytes", c_i64), ("layers8", ctypes.POINTER(LayerW8)), ("q8", c_vp), ("s8", c_vp),
-                ("resid_f32", c_int)]
+                ("resid_f32", c_int), ("gemm_x3", c_int), ("x3_ws", c_vp), ("x3_ws_bytes", c_i64)]
 
 
 P = ctypes.POINTER
 _lib.declare("clipmi_encoder_fwd", [c_vp, P(EncoderDesc)])
 _lib.declare("clipmi_encoder_bwd", [c_vp, P(EncoderDesc), c_vp])
 _lib.declare("clipmi_encoder_bwd_ws", [P(EncoderDesc)], c_i64)
+_lib.declare("clipmi_encoder_x3_ws", [P(EncoderDesc)], c_i64)
 _lib.declare("clipmi_encoder_bwd_layers", [c_vp, P(EncoderDesc), c_vp, c_int, c_int])
 _lib.declare("clipmi_layernorm_fwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                       c_float, c_vp, c_vp, c_int])
@@ -270,7 +271,9 @@ class Encoder:
         self._wcache["w8"] = (key, tab, keep)
         return tab
 
-    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None, fp8=False, resid32=False):
+    def desc(self, dtype, B, N, wbuf, acts, x_out, mask, grads=None, ws=None, fp8=False, resid32=False, x3=False):
+        """x3: the bf16x3 mode (fp32 encoder, every GEMM a split-operand bf16 product); its split-image
+        scratch is allocated here and lives as long as the returned descriptor (d.x3_keep)."""
         t = self.t
         d = EncoderDesc()
         d.dtype, d.B, d.N, d.D, d.F = dcode(dtype), B, N, t.hidden_size, t.intermediate_size
@@ -291,6 +294,10 @@ class Encoder:
         d.x_out = x_out
         if ws is not None:
             d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        if x3 and dtype == torch.float32:
+            d.gemm_x3 = 1
+            d.x3_keep = _ws(_lib.lib().clipmi_encoder_x3_ws(ctypes.byref(d)), self.arena.device)
+            d.x3_ws, d.x3_ws_bytes = d.x3_keep.data_ptr(), d.x3_keep.numel()
         return d
 
 
@@ -385,7 +392,8 @@ class VisionTowerFn(torch.autograd.Function):
         Wp = arena.view("vision_model.embeddings.patch_embedding.weight", wbuf).view(D, Kc)
         if Kp != Kc:
             Wp = torch.nn.functional.pad(Wp, (0, Kp - Kc))
-        K.gemm(R, D, Kp, X, Kp, True, Wp, Kp, True, h0, D)
+        x3 = getattr(rt, "x3", False)  # bf16x3 mode: the patch product split too
+        K.gemm(R, D, Kp, X, Kp, True, Wp, Kp, True, h0, D, split3=x3)
         buf, acts = rt.venc.alloc(B, N, dtype, dev, train, resid32=r32)
         stats0 = torch.empty(2, R, dtype=torch.float32, device=dev)
         call("clipmi_layernorm_fwd", s, dcode(xdtype), P_(h0), D, acts[0].x_in, D,
@@ -394,8 +402,9 @@ class VisionTowerFn(torch.autograd.Function):
              arena.ptr("vision_model.embeddings.position_embedding.weight", ebuf),
              arena.ptr("vision_model.embeddings.class_embedding", ebuf), N)
         out = torch.empty(B, N, D, dtype=xdtype, device=dev)
-        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None, fp8=fp8, resid32=r32)
+        d = rt.venc.desc(dtype, B, N, wbuf, acts, out.data_ptr(), None, fp8=fp8, resid32=r32, x3=x3)
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
+        del d
         if train:
             ctx.rt, ctx.B, ctx.buf, ctx.acts, ctx.X, ctx.h0, ctx.stats0 = rt, B, buf, acts, X, h0, stats0
             ctx.r32 = r32
@@ -415,11 +424,13 @@ class VisionTowerFn(torch.autograd.Function):
         arena.prepare_grads()
         wbuf = _wbuf(arena, dtype)
         dx = dout.to(dtype).contiguous().clone()
-        d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads(), resid32=ctx.r32)
+        x3 = getattr(rt, "x3", False)
+        d = rt.venc.desc(dtype, B, N, wbuf, ctx.acts, None, None, grads=rt.venc.grads(), resid32=ctx.r32, x3=x3)
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
         hook = _grad_hook(rt)
         rt.venc.backward(s, d, dx.data_ptr(), hook)
+        del d, ws  # the workspaces return to the stream-ordered pool
         # pre_layrnorm backward -> gradient of the embedding sum h0 (h0 fp32 with the fp32 residual stream;
         # the gradients stay in the activation dtype)
         dh0 = torch.empty(R, D, dtype=dtype, device=dev)
@@ -433,12 +444,17 @@ class VisionTowerFn(torch.autograd.Function):
         gW = arena.view("vision_model.embeddings.patch_embedding.weight", g).view(D, Kc)
         if Kp != Kc:  # padded patch K: accumulate the [D, Kp] product's first Kc columns
             gW_arena, gW = gW, torch.zeros(D, Kp, dtype=gW.dtype, device=dev)
-        splits = max(1, min(32, 1024 // max(1, ((D + 127) // 128) * ((Kp + 127) // 128))))
-        while splits > 1 and R // splits < 512:
-            splits -= 1
-        wsp = _ws(splits * D * Kp * 4, dev) if splits > 1 else None
+        if x3:  # the bf16 256-tile kernel over 3R: about one round of workgroups
+            splits = max(1, min(64, 256 // max(1, ((D + 255) // 256) * ((Kp + 255) // 256))))
+            while splits > 1 and 3 * R // splits < 512:
+                splits -= 1
+        else:
+            splits = max(1, min(32, 1024 // max(1, ((D + 127) // 128) * ((Kp + 127) // 128))))
+            while splits > 1 and R // splits < 512:
+                splits -= 1
+        wsp = _ws(splits * D * Kp * 4, dev) if splits > 1 and not x3 else None
         K.gemm(D, Kp, R, dh0, D, False, ctx.X, Kp, False, gW, Kp, flags=_lib.EPI_BETA, split_k=splits,
-               workspace=wsp)
+               workspace=wsp, split3=x3)
         if Kp != Kc:
             gW_arena.add_(gW[:, :Kc])
         call("clipmi_period_sum", s, dc, P_(dh0), D, B, N, N, D,
@@ -487,8 +503,10 @@ class TextTowerFn(torch.autograd.Function):
              arena.ptr("text_model.embeddings.position_embedding.weight", ebuf), acts[0].x_in, R, S, D, t.vocab_size,
              P_(bad))
         xL = torch.empty(R, D, dtype=xdtype, device=dev)
-        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask, fp8=fp8, resid32=r32)
+        d = rt.tenc.desc(dtype, B, S, wbuf, acts, xL.data_ptr(), mask, fp8=fp8, resid32=r32,
+                         x3=getattr(rt, "x3", False))
         _lib.check(_lib.lib().clipmi_encoder_fwd(s, ctypes.byref(d)), "clipmi_encoder_fwd")
+        del d
         out = torch.empty(B, S, D, dtype=dtype, device=dev)
         stats = torch.empty(2, R, dtype=torch.float32, device=dev)
         call("clipmi_layernorm_fwd2", s, dcode(xdtype), dc, P_(xL), D, P_(out), D,
@@ -518,11 +536,13 @@ class TextTowerFn(torch.autograd.Function):
              P_(ctx.stats[1]), arena.ptr("text_model.final_layer_norm.weight", wbuf), P_(dx), D, None, 0,
              arena.ptr("text_model.final_layer_norm.weight", g), arena.ptr("text_model.final_layer_norm.bias", g), 1,
              P_(lws), lws.numel(), R, D)
-        d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads(), resid32=ctx.r32)
+        d = rt.tenc.desc(dtype, B, S, wbuf, ctx.acts, None, ctx.mask, grads=rt.tenc.grads(), resid32=ctx.r32,
+                         x3=getattr(rt, "x3", False))
         ws = _ws(_lib.lib().clipmi_encoder_bwd_ws(ctypes.byref(d)), dev)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
         hook = _grad_hook(rt)
         rt.tenc.backward(s, d, dx.data_ptr(), hook)
+        del d, ws
         V = t.vocab_size
         ews = _ws(_lib.lib().clipmi_text_embed_bwd_ws(R, V), dev)
         call("clipmi_text_embed_bwd", s, dc, P_(ctx.ids), P_(dx), R, D, V,

@@ -45,10 +45,30 @@ namespace {
 size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
+// The bf16x3 mode's split-image scratch of the encoder call in progress on this thread (the engine only
+// enqueues work, so a call's GEMMs are issued by the calling thread between X3Scope's bounds).
+struct X3 {
+  void* ws;
+  int64_t bytes;
+};
+thread_local const X3* t_x3 = nullptr;
+struct X3Scope {
+  X3 x3;
+  explicit X3Scope(const clipmi_encoder_desc* d) : x3{d->x3_ws, d->x3_ws_bytes} {
+    t_x3 = (d->gemm_x3 && d->dtype == CLIPMI_F32) ? &x3 : nullptr;
+  }
+  ~X3Scope() { t_x3 = nullptr; }
+};
+
 int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb,
          bool bkm, void* C, int64_t ldc, int c_dt, int flags, const void* bias = nullptr, const void* res = nullptr,
          int64_t ldr = 0, void* aux = nullptr, int64_t ldaux = 0, int split = 1, void* ws = nullptr,
          int64_t ws_bytes = 0, float* bias_grad = nullptr) {
+  if (t_x3 && dt == CLIPMI_F32) {  // bf16x3: the split images (and any split-K slabs) in the x3 scratch
+    flags |= CLIPMI_GEMM_SPLIT3;
+    ws = t_x3->ws;
+    ws_bytes = t_x3->bytes;
+  }
   clipmi_gemm_desc d;
   memset(&d, 0, sizeof(d));
   d.M = M; d.N = N; d.K = K;
@@ -112,6 +132,27 @@ int wgrad_splits(int M, int N, int K, int dt) {
   return best;
 }
 
+// split-K factor of a wgrad GEMM in the encoder's mode (bf16x3: the bf16 kernel over 3R)
+int wgrad_splits_mode(const clipmi_encoder_desc* d, int M, int N, int R) {
+  if (d->gemm_x3 && d->dtype == CLIPMI_F32) return wgrad_splits(M, N, 3 * R, CLIPMI_BF16);
+  return wgrad_splits(M, N, R, d->dtype);
+}
+
+// bf16x3 scratch: the largest split-image set (+ split-K slabs) over the encoder's GEMMs
+int64_t x3_bytes(const clipmi_encoder_desc* d) {
+  if (!d->gemm_x3 || d->dtype != CLIPMI_F32) return 0;
+  const int R = d->B * d->N, D = d->D, F = d->F;
+  int64_t b = 0;
+  const int fw[4][2] = {{3 * D, D}, {D, D}, {F, D}, {D, F}};  // forward [N, K] (both operands k-major)
+  for (auto& f : fw) {
+    b = std::max(b, clipmi_gemm_split3_ws(R, f[0], f[1], 1, 1, 1));
+    b = std::max(b, clipmi_gemm_split3_ws(R, f[1], f[0], 1, 0, 1));  // the input gradient of the same layer
+  }
+  const int wg[4][2] = {{D, F}, {F, D}, {D, D}, {3 * D, D}};
+  for (auto& w : wg) b = std::max(b, clipmi_gemm_split3_ws(w[0], w[1], R, 0, 0, wgrad_splits_mode(d, w[0], w[1], R)));
+  return b;
+}
+
 struct WsPlan {
   int64_t g2, dln, dbig, split, colsum, ln, total;
 };
@@ -128,7 +169,7 @@ WsPlan plan(const clipmi_encoder_desc* d) {
   int64_t sp = 0;
   const int shapes[4][2] = {{d->F, d->D}, {d->D, d->F}, {d->D, d->D}, {3 * d->D, d->D}};
   for (auto& sh : shapes) {
-    const int s = wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
+    const int s = (d->gemm_x3 && d->dtype == CLIPMI_F32) ? 1 : wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
     if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * (sh[1] + 1) * 4);  // slabs + bias partials
   }
   p.colsum = p.split + align256(sp);
@@ -170,18 +211,23 @@ int validate(const clipmi_encoder_desc* d) {
                  "fp8 encoder: hidden size must be a multiple of 256 and the MLP width of 128");
   CLIPMI_REQUIRE(d->D == d->H * 64, "hidden size must be heads * 64");
   CLIPMI_REQUIRE(d->B >= 0 && d->N >= 1 && d->L >= 1, "shape");
+  CLIPMI_REQUIRE(!d->gemm_x3 || d->dtype == CLIPMI_F32, "gemm_x3 needs the fp32 encoder");
+  CLIPMI_REQUIRE(!d->gemm_x3 || (d->x3_ws && d->x3_ws_bytes >= x3_bytes(d) && ((uintptr_t)d->x3_ws & 255) == 0),
+                 "gemm_x3: x3_ws too small or not 256-byte aligned (clipmi_encoder_x3_ws)");
   return CLIPMI_OK;
 }
 
 }  // namespace
 
 extern "C" int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d) { return plan(d).total; }
+extern "C" int64_t clipmi_encoder_x3_ws(const clipmi_encoder_desc* d) { return d ? x3_bytes(d) : 0; }
 
 extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
   CLIPMI_TRY(validate(d));
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
+  X3Scope x3(d);
   if (dt == CLIPMI_FP8) {  // BASELINE config 5: frozen towers, MXFP8 GEMMs, bf16 everything else
     const int bf = CLIPMI_BF16;
     // scratch: [R, D] operand (LayerNorm / attention outputs) then [R, F] (fc1 output), each with its scales
@@ -260,6 +306,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   if (R == 0) return CLIPMI_OK;
   const WsPlan p = plan(d);
   CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= p.total, "encoder_bwd workspace too small");
+  X3Scope x3(d);
   char* ws = (char*)d->workspace;
   void* g2 = ws + p.g2;
   void* dln = ws + p.dln;
@@ -275,7 +322,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
   auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                    float* bgrad) -> int {
-    const int sp = wgrad_splits(M, N, R, dt);
+    const int sp = wgrad_splits_mode(d, M, N, R);
     const bool fuse = dt == CLIPMI_BF16;
     CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
                     nullptr, 0, sp, wsplit, split_bytes, fuse ? bgrad : nullptr));

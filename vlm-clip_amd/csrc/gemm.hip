@@ -1243,6 +1243,17 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
       case E_B: launch256<true, true, float, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias_f32";
       case E_B | E_R: launch256<true, true, float, E_B | E_R, false>(p, splits, s, bg); return "gemm256_fwd_bias_resid_f32";
       case 0: launch256<true, true, float, 0, false>(p, splits, s, bg); return "gemm256_fwd_f32";
+      // the bf16x3 mode's fc1 (training: the derivative stored beside the activation; inference)
+      case E_B | E_Q | E_DA: launch256<true, true, float, E_B | E_Q | E_DA, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu_dact_f32";
+      case E_B | E_Q: launch256<true, true, float, E_B | E_Q, false>(p, splits, s, bg); return "gemm256_fwd_bias_qgelu_f32";
+      default: break;
+    }
+  }
+  // the bf16x3 mode's input gradients (fp32 gradients; fc2's with the stored-derivative product)
+  if (f32o && !p.ws && splits == 1 && sel == 2) {
+    switch (flags) {
+      case 0: launch256<true, false, float, 0, false>(p, splits, s, bg); return "gemm256_dgrad_f32";
+      case E_MA: launch256<true, false, float, E_MA, false>(p, splits, s, bg); return "gemm256_dgrad_mulaux_f32";
       default: break;
     }
   }
@@ -1374,6 +1385,107 @@ extern "C" int clipmi_gemm_batched(void* stream, const clipmi_gemm_desc* d, int 
   return CLIPMI_OK;
 }
 
+// ------------------------------------------------------------------ bf16x3 split-operand fp32 GEMM
+// An fp32 product on the bf16 MFMA kernels (precision "bf16x3", the fast mode that meets north_star's
+// 1e-3 logits): each fp32 operand is split as x = xh + xl with xh = bf16(x), xl = bf16(x - xh) (16
+// significant bits between them), and A.B^T ~ Ah.Bh^T + Ah.Bl^T + Al.Bh^T -- the dropped Al.Bl^T is
+// ~2^-16 of each product (profiles/r05_bf16x3_precision.log: max |dlogit| 1-2e-4 at config 3).  The
+// three products run as ONE bf16 GEMM over a reduction axis of length 3K on concatenated operands
+//   A3 = [Ah | Ah | Al],  B3 = [Bh | Bl | Bh]
+// (k-major operands: column blocks of width K; operands row-major in k: row blocks of height K), every
+// bf16 x bf16 product exact in the fp32 accumulator, so the 256-tile kernels and their epilogues (bias,
+// activations, residual, aux, beta, split-K slabs) apply unchanged with fp32 C.  The split images live
+// in the caller's workspace (clipmi_gemm_split3_ws); one pass per operand reads 4 B and writes 6 B per
+// element.
+//   pattern 0 (A): segments h, h, l;  pattern 1 (B): h, l, h.
+// One workgroup per source row (nr rows of nc elements), V elements per thread step.
+template <int V>
+__global__ __launch_bounds__(256) void split3_kernel(const float* X, int64_t ldx, int nc, bf16* out, int64_t ldo,
+                                                     int64_t seg, int pattern) {
+  const int64_t r = blockIdx.x;
+  const float* x = X + r * ldx;
+  bf16* o = out + r * ldo;
+  for (int c = threadIdx.x * V; c < nc; c += 256 * V) {
+    float v[V];
+    if constexpr (V == 4) {
+      const f32x4 t = *(const f32x4*)(x + c);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+      v[0] = x[c];
+    }
+    bf16 h[V], l[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      h[j] = (bf16)v[j];
+      l[j] = (bf16)(v[j] - (float)h[j]);
+    }
+    auto put = [&](bf16* q, const bf16 (&w)[V]) {
+      if constexpr (V == 4) *(bf16x4*)q = bf16x4{w[0], w[1], w[2], w[3]};
+      else q[0] = w[0];
+    };
+    put(o + c, h);
+    put(o + seg + c, pattern ? l : h);
+    put(o + 2 * seg + c, pattern ? h : l);
+  }
+}
+
+namespace {
+// the split image of one operand: k-major [rows][3K] (ld 3K), else [3K][round8(rows)]
+int64_t split3_elems(int rows, int K, bool kmajor) {
+  return kmajor ? (int64_t)rows * 3 * K : (int64_t)3 * K * ((rows + 7) / 8 * 8);
+}
+int64_t al256b(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+int split3_operand(hipStream_t s, const float* X, int64_t ldx, int rows, int K, bool kmajor, bf16* out, int pattern) {
+  // k-major: X[r][k] (rows x K) -> out[r][j K + k];  row-major in k: X[k][r] (K x rows) -> out[j K + k][r]
+  const int nr = kmajor ? rows : K, nc = kmajor ? K : rows;
+  const int64_t ldo = kmajor ? (int64_t)3 * K : (rows + 7) / 8 * 8;
+  const int64_t seg = kmajor ? (int64_t)K : (int64_t)K * ldo;
+  if (nr == 0 || nc == 0) return CLIPMI_OK;
+  const bool v4 = nc % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 && ldo % 4 == 0;
+  if (v4) hipLaunchKernelGGL(split3_kernel<4>, dim3(nr), dim3(256), 0, s, X, ldx, nc, out, ldo, seg, pattern);
+  else hipLaunchKernelGGL(split3_kernel<1>, dim3(nr), dim3(256), 0, s, X, ldx, nc, out, ldo, seg, pattern);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+int gemm_split3(hipStream_t s, const clipmi_gemm_desc* d) {
+  CLIPMI_REQUIRE(d->ab_dtype == CLIPMI_F32 && d->c_dtype == CLIPMI_F32, "split3: fp32 operands and output");
+  CLIPMI_REQUIRE(!d->bias_grad, "split3: the fused bias gradient would sum the split image (use clipmi_colsum)");
+  CLIPMI_REQUIRE((!d->a_kmajor && !d->b_kmajor) || d->K % 8 == 0, "split3: K % 8 == 0 with a k-major operand");
+  CLIPMI_REQUIRE(d->A && d->B, "split3: operands");
+  const int64_t need = clipmi_gemm_split3_ws(d->M, d->N, d->K, d->a_kmajor, d->b_kmajor, d->split_k);
+  CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= need && ((uintptr_t)d->workspace & 255) == 0,
+                 "split3: workspace too small or not 256-byte aligned (clipmi_gemm_split3_ws)");
+  if (d->M == 0 || d->N == 0) return CLIPMI_OK;
+  char* w = (char*)d->workspace;
+  const int64_t a_bytes = al256b(split3_elems(d->M, d->K, d->a_kmajor) * 2);
+  const int64_t b_bytes = al256b(split3_elems(d->N, d->K, d->b_kmajor) * 2);
+  bf16* A3 = (bf16*)w;
+  bf16* B3 = (bf16*)(w + a_bytes);
+  CLIPMI_TRY(split3_operand(s, (const float*)d->A, d->lda, d->M, d->K, d->a_kmajor, A3, 0));
+  CLIPMI_TRY(split3_operand(s, (const float*)d->B, d->ldb, d->N, d->K, d->b_kmajor, B3, 1));
+  clipmi_gemm_desc e = *d;
+  e.flags &= ~CLIPMI_GEMM_SPLIT3;
+  e.ab_dtype = CLIPMI_BF16;
+  e.K = 3 * d->K;
+  e.A = A3;
+  e.lda = d->a_kmajor ? (int64_t)3 * d->K : (d->M + 7) / 8 * 8;
+  e.B = B3;
+  e.ldb = d->b_kmajor ? (int64_t)3 * d->K : (d->N + 7) / 8 * 8;
+  e.workspace = w + a_bytes + b_bytes;
+  e.workspace_bytes = d->workspace_bytes - a_bytes - b_bytes;
+  return clipmi_gemm((void*)s, &e);
+}
+}  // namespace
+
+extern "C" int64_t clipmi_gemm_split3_ws(int M, int N, int K, int a_kmajor, int b_kmajor, int split_k) {
+  if (M < 0 || N < 0 || K < 0) return 0;
+  int64_t b = al256b(split3_elems(M, K, a_kmajor) * 2) + al256b(split3_elems(N, K, b_kmajor) * 2);
+  if (split_k > 1) b += (int64_t)split_k * M * N * 4;
+  return b;
+}
+
 extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
@@ -1386,7 +1498,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_BIAS) || d->bias, "bias flag needs bias");
     CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_STORE_DACT) || (d->flags & (CLIPMI_EPI_QGELU | CLIPMI_EPI_GELU)),
                    "store_dact needs an activation flag");
-    CLIPMI_REQUIRE((d->flags & ~1023) == 0, "unknown epilogue flag");
+    CLIPMI_REQUIRE((d->flags & ~(1023 | CLIPMI_GEMM_SPLIT3)) == 0, "unknown epilogue flag");
     // aux has one role per launch, and the epilogues read one input stream besides it
     constexpr int AUXR = CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU | CLIPMI_EPI_MUL_AUX;
     constexpr int AUXW = CLIPMI_EPI_STORE_PRE | CLIPMI_EPI_STORE_DACT;
@@ -1396,6 +1508,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     CLIPMI_REQUIRE(!((d->flags & CLIPMI_EPI_MUL_AUX) && (d->flags & (CLIPMI_EPI_RESID | CLIPMI_EPI_BETA))),
                    "mul_aux cannot be combined with residual / beta");
   }
+  if (d->flags & CLIPMI_GEMM_SPLIT3) return gemm_split3(s, d);
   if (d->ab_dtype == CLIPMI_FP8) {  // MXFP8 operands (see include/clipmi.h)
     CLIPMI_REQUIRE(d->a_kmajor && d->b_kmajor, "fp8: both operands k-major");
     CLIPMI_REQUIRE(d->K % 128 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0, "fp8: K % 128 == 0, lda/ldb % 16 == 0");
