@@ -172,6 +172,9 @@ WsPlan plan(const clipmi_encoder_desc* d) {
     const int s = (d->gemm_x3 && d->dtype == CLIPMI_F32) ? 1 : wgrad_splits(sh[0], sh[1], (int)R, d->dtype);
     if (s > 1) sp = std::max<int64_t>(sp, (int64_t)s * sh[0] * (sh[1] + 1) * 4);  // slabs + bias partials
   }
+  // bf16: two slab regions used alternately, so a weight gradient's split-K sum can be deferred into the
+  // next persistent GEMM while the following weight gradient writes its own slabs (DeferredReduce)
+  if (d->dtype == CLIPMI_BF16) sp = 2 * align256(sp);
   p.colsum = p.split + align256(sp);
   p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));
   p.total = p.ln + align256(clipmi_layernorm_bwd_ws((int)R, d->D));
@@ -318,15 +321,36 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   const int64_t col_bytes = p.ln - p.colsum;
   const int64_t ln_bytes = p.total - p.ln;
   const int f32 = CLIPMI_F32;
+  // bf16: the second stages of the split-K weight gradients and of the LayerNorm affine gradients are
+  // deferred into the next persistent GEMM launch (internal.h DeferredReduce; at most one outstanding,
+  // the rest launch as usual), the last one launched at the end of this call
+  DeferredReduce pend;
+  memset(&pend, 0, sizeof(pend));
+  const char* denv = getenv("CLIPMI_DEFER");  // 0: launch every reduction on its own (A/B, bitwise test)
+  struct Slot {
+    explicit Slot(DeferredReduce* r) { deferred_slot() = r; }
+    ~Slot() { deferred_slot() = nullptr; }
+  } slot(dt == CLIPMI_BF16 && !(denv && denv[0] == '0') ? &pend : nullptr);
+  const int64_t region = dt == CLIPMI_BF16 ? split_bytes / 2 : split_bytes;
+  int wg_no = 0;
   // wgrad: C[M,N] += sum_tokens A[t][m] B[t][n]; the bf16 path also fuses the Linear bias
   // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
   auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                    float* bgrad) -> int {
     const int sp = wgrad_splits_mode(d, M, N, R);
     const bool fuse = dt == CLIPMI_BF16;
+    char* wsl = (char*)wsplit + (dt == CLIPMI_BF16 ? (wg_no++ & 1) * region : 0);
+    // an outstanding split-K sum still reading this region runs first (not reached with the alternation)
+    if (pend.kind == 1 && (const char*)pend.ws >= wsl && (const char*)pend.ws < wsl + region)
+      CLIPMI_TRY(launch_deferred((hipStream_t)s, pend));
     CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
-                    nullptr, 0, sp, wsplit, split_bytes, fuse ? bgrad : nullptr));
+                    nullptr, 0, sp, wsl, region, fuse ? bgrad : nullptr));
     if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
+    return CLIPMI_OK;
+  };
+  // LayerNorm backward rewrites the partial rows an outstanding affine sum reads: run that one first
+  auto ln_guard = [&]() -> int {
+    if (pend.kind == 2) CLIPMI_TRY(launch_deferred((hipStream_t)s, pend));
     return CLIPMI_OK;
   };
   for (int l = layer_hi - 1; l >= layer_lo; --l) {
@@ -340,6 +364,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     CLIPMI_TRY(wgrad(D, F, dx, D, a.act, F, g.fc2_w, g.fc2_b));            // gW2 += dx^T act, gb2 += sum dx
     CLIPMI_TRY(wgrad(F, D, dbig, F, a.ln2, D, g.fc1_w, g.fc1_b));          // gW1 += d_pre^T ln2
     CLIPMI_TRY(gemm(s, dt, R, D, F, dbig, F, true, w.fc1_w, D, false, dln, D, dt, 0));  // d_ln2 = d_pre W1
+    CLIPMI_TRY(ln_guard());
     CLIPMI_TRY(clipmi_layernorm_bwd2(s, xdt, dt, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx, D, g.ln2_w,
                                      g.ln2_b, 1, wln, ln_bytes, R, D));   // dh = dx + LN2'(d_ln2)
     // attention branch: g2 is dL/dh
@@ -349,8 +374,10 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
                                     d->N, D));                              // d_qkv
     CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w, g.qkv_b));  // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
+    CLIPMI_TRY(ln_guard());
     CLIPMI_TRY(clipmi_layernorm_bwd2(s, xdt, dt, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D, g2, D, g.ln1_w,
                                      g.ln1_b, 1, wln, ln_bytes, R, D));    // dx_in = dh + LN1'(d_ln1)
   }
+  if (pend.kind != 0) CLIPMI_TRY(launch_deferred((hipStream_t)s, pend));  // this call's gradients are final
   return CLIPMI_OK;
 }

@@ -1661,11 +1661,14 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     const int64_t total = (int64_t)d->M * d->N;
     const int beta = (d->flags & CLIPMI_EPI_BETA) ? 1 : 0;
     if (d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0 && ((uintptr_t)p.ws & 15) == 0) {
-      const int nblk = (int)std::min<int64_t>((total / 4 + 255) / 256, 65536);
-      const int nbias = p.bws ? (d->M + 255) / 256 : 0;
-      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(nblk + nbias), dim3(256), 0, s,
-                         p.ws, (float*)d->C, d->ldc, d->M, d->N, splits, d->alpha, beta, nblk, (const float*)p.bws,
-                         d->bias_grad);
+      DeferredReduce r;
+      memset(&r, 0, sizeof(r));
+      r.kind = 1;
+      r.ws = p.ws; r.C = (float*)d->C; r.ldc = d->ldc; r.M = d->M; r.N = d->N; r.splits = splits;
+      r.alpha = d->alpha; r.beta = beta; r.bws = p.bws; r.bias_grad = d->bias_grad;
+      DeferredReduce* slot = deferred_slot();
+      if (slot && slot->kind == 0) *slot = r;  // executed by the next persistent GEMM launch
+      else CLIPMI_TRY(launch_deferred(s, r));
     } else {
       const unsigned nblk = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk), dim3(256), 0, s,
@@ -1676,6 +1679,26 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     }
     CLIPMI_CHECK_LAUNCH();
   }
+  return CLIPMI_OK;
+}
+
+DeferredReduce*& deferred_slot() {
+  static thread_local DeferredReduce* slot = nullptr;
+  return slot;
+}
+
+int launch_deferred(hipStream_t s, DeferredReduce& r) {
+  if (r.kind == 1) {
+    const int64_t total = (int64_t)r.M * r.N;
+    const int nblk = (int)std::min<int64_t>((total / 4 + 255) / 256, 65536);
+    const int nbias = r.bws ? (r.M + 255) / 256 : 0;
+    hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(nblk + nbias), dim3(256), 0, s, r.ws, r.C, r.ldc, r.M, r.N, r.splits,
+                       r.alpha, r.beta, nblk, r.bws, r.bias_grad);
+    CLIPMI_CHECK_LAUNCH();
+  } else if (r.kind == 2) {
+    CLIPMI_TRY(launch_partials_reduce(s, r));
+  }
+  r.kind = 0;
   return CLIPMI_OK;
 }
 

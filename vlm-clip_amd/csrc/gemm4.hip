@@ -391,6 +391,141 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4_kernel(GemmP p) {
 #define W4P_ST(ph) do { } while (0)
 #endif
 
+// A deferred reduction (internal.h DeferredReduce) shared by the launch's workgroups before their first
+// item, with the arithmetic and summation order of the standalone kernels (splitk_reduce4_kernel,
+// reduce_partials4_kernel), so the results are bitwise the same.  lds: 4 KiB of scratch (the epilogue
+// staging area, idle until the first epilogue).  Every thread of the workgroup calls it.
+__device__ __forceinline__ void hosted_reduce(const DeferredReduce& r, char* lds, int wg, int nwg, int t) {
+  // One wave per SIMD has little latency hiding of its own: every thread keeps 16 slab loads in flight
+  // (4 column groups x 4 splits), then adds them in split order per group, as the standalone kernel does.
+  if (r.kind == 1) {
+    const int64_t total = (int64_t)r.M * r.N;
+    const int n4 = r.N >> 2;
+    const int64_t total4 = (int64_t)r.M * n4;
+    const int64_t step = (int64_t)nwg * 256;
+    for (int64_t i0 = (int64_t)wg * 256 + t; i0 < total4; i0 += 4 * step) {
+      int64_t off[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * step;
+        ok[u] = i < total4;
+        const int m = ok[u] ? (int)(i / n4) : 0, n = ok[u] ? (int)(i - (int64_t)m * n4) * 4 : 0;
+        off[u] = (int64_t)m * r.N + n;
+      }
+      float4 sum[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sum[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      // straight-line loads (invalid groups read offset 0 and are never stored), so all 16 are in flight
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (!ok[u]) off[u] = 0;
+      int z = 0;
+      for (; z + 4 <= r.splits; z += 4) {
+        float4 v[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[j][u] = *(const float4*)(r.ws + off[u] + (int64_t)(z + j) * total);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            sum[u].x += v[j][u].x; sum[u].y += v[j][u].y; sum[u].z += v[j][u].z; sum[u].w += v[j][u].w;
+          }
+      }
+      for (; z < r.splits; ++z) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(r.ws + off[u] + (int64_t)z * total);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          sum[u].x += v[u].x; sum[u].y += v[u].y; sum[u].z += v[u].z; sum[u].w += v[u].w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!ok[u]) continue;
+        const int64_t m = off[u] / r.N, n = off[u] - m * r.N;
+        float4* c = (float4*)(r.C + m * r.ldc + n);
+        float4 o = make_float4(r.alpha * sum[u].x, r.alpha * sum[u].y, r.alpha * sum[u].z, r.alpha * sum[u].w);
+        if (r.beta) {
+          const float4 q = *c;
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        *c = o;
+      }
+    }
+    if (r.bws) {
+      for (int m = wg * 256 + t; m < r.M; m += nwg * 256) {
+        float acc = 0.f;
+        int z = 0;
+        for (; z + 8 <= r.splits; z += 8) {  // 8 loads in flight, added in split order
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = r.bws[(int64_t)(z + j) * r.M + m];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += v[j];
+        }
+        for (; z < r.splits; ++z) acc += r.bws[(int64_t)z * r.M + m];
+        r.bias_grad[m] += acc;
+      }
+    }
+    return;
+  }
+  // kind 2: 16-column chunks (four lanes x four columns; one chunk per workgroup, so 2D / 16 of them share
+  // the work); each of the standalone kernel's 64 partial groups ty (partials ty, ty + 64, ..., in order) is
+  // one thread here (t >> 2), 8 of its loads in flight, then the kernel's tree: groups of 4, then 16 in order
+  const int Dt = r.out2 ? 2 * r.D : r.D;
+  const int nch = (Dt + 15) / 16;
+  float4* red = (float4*)lds;  // [64 groups][4 lanes]
+  const int tx = t & 3, ty = t >> 2;
+  for (int ch = wg; ch < nch; ch += nwg) {
+    const int c = ch * 16 + tx * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < Dt) {
+      const float* src = r.part + c;
+      int p = ty;
+      for (; p + 7 * 64 < r.P; p += 8 * 64) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const float4*)(src + (int64_t)(p + j * 64) * r.stride);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
+        }
+      }
+      for (; p < r.P; p += 64) {
+        const float4 v = *(const float4*)(src + (int64_t)p * r.stride);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    *LDS_PTR(f32x4, (char*)(red + ty * 4 + tx)) = f32x4{acc.x, acc.y, acc.z, acc.w};
+    __syncthreads();
+    if (ty == 0 && c < Dt) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const f32x4 a0 = *LDS_PTR(const f32x4, (char*)(red + (4 * q) * 4 + tx));
+        float4 a = make_float4(a0[0], a0[1], a0[2], a0[3]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const f32x4 b = *LDS_PTR(const f32x4, (char*)(red + (4 * q + k) * 4 + tx));
+          a.x += b[0]; a.y += b[1]; a.z += b[2]; a.w += b[3];
+        }
+        if (q == 0) s = a;
+        else { s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w; }
+      }
+      float* o = c < r.D ? r.out + c : r.out2 + (c - r.D);
+      if (r.pbeta) {
+        s.x += o[0]; s.y += o[1]; s.z += o[2]; s.w += o[3];
+      }
+      o[0] = s.x; o[1] = s.y; o[2] = s.z; o[3] = s.w;
+    }
+    __syncthreads();
+  }
+}
+
 // PF: L2 prefetch of the streamed operands (A always; B too for the weight gradient, whose B is the
 // activation X) PF_D stages ahead, issued after each second half-step's DMAs (w4_prefetch); the next
 // sync then waits vmcnt(NPF) so the prefetch stays in flight, and a prefetch is required complete
@@ -415,7 +550,7 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   const int splits = (p.K + p.k_per_split - 1) / p.k_per_split;
   const int nitems = p.ntiles * max(1, splits);
   int item = xcd_remap(blockIdx.x, nwg);
-  if (item >= nitems) return;
+  if (item >= nitems && p.red.kind == 0) return;
   const int lda = (int)p.lda, ldb = (int)p.ldb;
   const W4Lane w = w4_lane<AK, BKM>(wave, lane, p.lda, p.ldb);
   auto coords = [&](int it, int& m0, int& n0, int& kz, int& kbeg, int& kend) {
@@ -439,7 +574,13 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
   if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   }
-  prologue_dma(item);
+  if (item < nitems) prologue_dma(item);
+  // a deferred reduction (the previous weight gradient's split-K sum or LayerNorm affine sum) while the
+  // first stages land
+  if (p.red.kind != 0) {
+    hosted_reduce(p.red, smem + 2 * W4_STAGE, blockIdx.x, nwg, t);
+    if (item >= nitems) return;
+  }
   f32x4 acc[2][8][4];
   f32x4 accb[8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
@@ -538,8 +679,15 @@ template <bool AK, bool BKM, typename OutT, int EPI, bool BG, bool PF = false>
 void launch_w4p(const GemmP& p, int splits, hipStream_t s, float* bias_grad) {
   constexpr int L = 2 * W4_STAGE + 4 * 8192;
   (void)lds_optin((const void*)gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, PF>, L);
-  const int grid = std::min(p.ntiles * splits, num_cus_w4());
-  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, PF>), dim3(grid), dim3(W4_THR), L, s, p, bias_grad);
+  int grid = std::min(p.ntiles * splits, num_cus_w4());
+  GemmP q = p;
+  DeferredReduce* slot = deferred_slot();
+  if (slot && slot->kind != 0) {  // host the recorded reduction (every CU's workgroup takes a share)
+    q.red = *slot;
+    slot->kind = 0;
+    grid = num_cus_w4();
+  }
+  hipLaunchKernelGGL((gemm_w4p_kernel<AK, BKM, OutT, EPI, BG, PF>), dim3(grid), dim3(W4_THR), L, s, q, bias_grad);
 }
 
 // dm: 100 persistent, 102 persistent with the L2 prefetch; experiments build only:

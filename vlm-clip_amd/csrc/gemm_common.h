@@ -36,6 +36,7 @@ struct GemmP {
   // i1 * s?1 + i2 * s?2 elements (nb2 == 0: no batch)
   int nb2;
   int64_t bsa1, bsa2, bsb1, bsb2, bsc1, bsc2;
+  DeferredReduce red;  // persistent 4-wave kernel: a deferred reduction its workgroups run first (kind 0: none)
 };
 
 // host side: the stamp buffer armed by clipmi_gemm_stamps (nullptr when disarmed)

@@ -41,3 +41,27 @@ struct ProfScope {
   ProfScope(hipStream_t stream, const char* label, double flops);
   void finish(const char* label, double flops);
 };
+
+// ---- deferred deterministic reductions (engine backward, bf16 path).  The second stage of a split-K
+// weight gradient (fp32 slabs -> C, per-split bias partials -> bias_grad) or of a LayerNorm affine
+// gradient (per-block partial rows -> dgamma / dbeta) is recorded instead of launched and executed by the
+// workgroups of the next persistent 4-wave GEMM launch on the same stream, before their first item
+// (gemm4.hip hosted_reduce): no launch of its own, so no reduce waits for CUs behind the other tower's
+// persistent GEMMs.  Same arithmetic, same order as the standalone kernels (bitwise equal).
+struct DeferredReduce {
+  int kind;  // 0 none, 1 split-K slabs, 2 column partials
+  // kind 1: C[m][n] = (beta ? C[m][n] : 0) + alpha * sum_z ws[z][m][n] (N % 4 == 0, 16-B aligned);
+  //         bias_grad[m] += sum_z bws[z][m] when bws
+  const float* ws; float* C; int64_t ldc; int M, N, splits; float alpha; int beta;
+  const float* bws; float* bias_grad;
+  // kind 2: column c < Dt of sum_p part[p * stride + c] -> out[c] (c < D) / out2[c - D] (+= when pbeta);
+  //         Dt = out2 ? 2D : D, D % 4 == 0
+  const float* part; int64_t stride; int P, D; float* out; float* out2; int pbeta;
+};
+// The calling thread's deferral slot (nullptr: reductions launch as usual).  An empty slot (kind 0) takes
+// the next split-K / LayerNorm second stage; a persistent 4-wave bf16 GEMM launch executes a recorded one
+// and empties the slot.
+DeferredReduce*& deferred_slot();
+// launch a recorded reduction on its own (the standalone kernels) and empty it
+int launch_deferred(hipStream_t s, DeferredReduce& r);
+int launch_partials_reduce(hipStream_t s, const DeferredReduce& r);  // kind 2 (norm.hip)

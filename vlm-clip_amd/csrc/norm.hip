@@ -11,6 +11,7 @@
 // two-pass variance from registers (no E[x^2]-E[x]^2 cancellation).
 #include "common.h"
 #include "internal.h"
+#include <cstring>
 
 namespace {
 
@@ -748,12 +749,26 @@ extern "C" int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const
   if (((uintptr_t)wsf & 15) != 0 || D % 4 != 0) {
     if (dw) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, beta_wb);
     if (db) hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, beta_wb);
-  } else if (dw && db)
-    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, db, beta_wb);
-  else if (dw)
+  } else if (dw && db) {
+    DeferredReduce r;
+    memset(&r, 0, sizeof(r));
+    r.kind = 2;
+    r.part = wsf; r.stride = (int64_t)2 * D; r.P = nb; r.D = D; r.out = dw; r.out2 = db; r.pbeta = beta_wb;
+    DeferredReduce* slot = deferred_slot();
+    if (slot && slot->kind == 0) *slot = r;  // executed by the next persistent GEMM launch (engine backward)
+    else CLIPMI_TRY(launch_partials_reduce(s, r));
+  } else if (dw)
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, (float*)nullptr, beta_wb);
   else if (db)
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, (float*)nullptr, beta_wb);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+int launch_partials_reduce(hipStream_t s, const DeferredReduce& r) {
+  const int Dt = r.out2 ? 2 * r.D : r.D;
+  hipLaunchKernelGGL(reduce_partials4_kernel, dim3((Dt + 63) / 64), dim3(1024), 0, s, r.part, r.stride, r.P, r.D, r.out,
+                     r.out2, r.pbeta);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
