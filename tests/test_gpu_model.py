@@ -62,6 +62,23 @@ def test_forward_matches_reference(golden, precision, tag, preset, B, adapters):
     assert np.abs(out["image_features"].cpu().numpy() - g["image_features"]).max() < fe
 
 
+@pytest.mark.parametrize("tag,preset,B,adapters", [("b32", "B/32", 8, True), ("l14", "L/14", 2, True)])
+def test_frozen_towers_fp32_residual_forward(golden, tag, preset, B, adapters):
+    """residual_fp32=True on frozen towers (the default only when the towers are trained): the bf16 mode
+    with the fp32 residual stream against the reference goldens, at a tighter bound than the bf16-residual
+    forward's 0.15."""
+    g = golden(f"forward_{tag}.npz")
+    m = CLIPWithAdapters(preset, use_text_adapter=adapters, use_vision_adapter=adapters, use_shared_adapters=False,
+                         freeze_clip=True, device="cuda", precision="bf16", residual_fp32=True)
+    assert m._rt.resid32
+    with torch.no_grad():
+        out = m(**batch(m.config, B, g))
+    torch.cuda.synchronize()
+    err = np.abs(out["logits_per_text"].cpu().numpy() - g["logits_per_text"]).max()
+    print(f"\n[{tag} bf16 fp32-residual] max|dlogit|={err:.4g}")
+    assert err < 0.10, err
+
+
 def test_eos_pooling_fp32(golden):
     g = golden("forward_b32_noadapter.npz")
     m = CLIPWithAdapters("B/32", use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,

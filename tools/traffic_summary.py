@@ -20,7 +20,11 @@ FAMILIES = {
 # r03 forward + dgrad launches per step in program order (CLIPMI_OVERLAP=0): text forward 48, the
 # patch embedding + vision forward 48, a 12-tile projection product, vision backward 48, an 8-tile
 # one, text backward 48 -- the vision tower's are positions 48 .. 145
-FD_PER_STEP, FD_VISION = 195, (48, 146)
+# r05 (fp32 residual stream: the patch embedding and the projections' forward are fp32-output launches of
+# their own): text forward 48, text projection, patch embedding, vision forward 48, visual projection,
+# a projection input gradient, vision backward 48, the text projection's, text backward 48 = 197; the
+# vision tower's are positions 49 .. 147 (patch embedding .. vision backward, as r03's 48 .. 145)
+FD_PER_STEP, FD_VISION = 197, (49, 148)
 # r03: 99 wgrad launches per step -- a projection's (grid 6), the vision tower's 48 encoder wgrads +
 # the patch embedding, the text projection's (grid 4), the text tower's 48 (r02: 97, vision first)
 PER_STEP, VISION0, VISION, M_TILES = 99, 1, 49, 788

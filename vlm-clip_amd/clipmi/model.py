@@ -5,10 +5,12 @@ checkpoint format and error types as the reference; the compute runs on libclipm
 (``clipmi.towers``).  Extensions, all keyword-only:
 
   device       where the fp32 parameter arenas live (default: cuda if available)
-  precision    "bf16" (MFMA path, default; fp32 residual stream), "fp32" (exact-f32 parity mode),
+  precision    "bf16" (MFMA path, default), "fp32" (exact-f32 parity mode),
                "bf16x3" (fp32 activations with the towers' GEMMs as bf16x3 split products on the MFMA
                kernels: north_star's 1e-3 logits at several times the fp32 mode's speed) or "fp8" (frozen
                towers with MXFP8 GEMMs, BASELINE config 5; adapters and the loss stay bf16 / fp32)
+  residual_fp32  bf16 mode: keep the towers' residual stream (each layer's input, the attention-branch sum)
+               in fp32 -- default when the towers are trained (freeze_clip=False), bf16 when they are frozen
   pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
                (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
   init_seed    seed of the deterministic random init used when no weights file exists
@@ -78,7 +80,7 @@ class CLIPWithAdapters(nn.Module):
     def __init__(self, clip_model_name="openai/clip-vit-base-patch32", text_adapter_size=256,
                  vision_adapter_size=256, shared_adapter_layers=2, freeze_clip=True, use_text_adapter=True,
                  use_vision_adapter=True, use_shared_adapters=True, *, device=None, precision="bf16",
-                 pooling="first", init_seed=0, process_group=None, fast_init=False):
+                 pooling="first", init_seed=0, process_group=None, fast_init=False, residual_fp32=None):
         super().__init__()
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
@@ -128,7 +130,11 @@ class CLIPWithAdapters(nn.Module):
         self._rt = _Runtime(self.clip, dtype)
         self._rt.fp8 = precision == "fp8"
         # bf16 mode: the towers' residual stream in fp32 (engine resid_f32; profiles/r05_bf16_error_sources.log)
-        self._rt.resid32 = precision == "bf16"
+        # when the towers are trained (full fine-tune, BASELINE config 3); frozen towers (the adapter configs)
+        # keep it in bf16, where the fp32 stream's 12 extra bytes per element and layer cost 7 % of the step
+        if residual_fp32 is None:
+            residual_fp32 = not freeze_clip
+        self._rt.resid32 = precision == "bf16" and bool(residual_fp32)
         # bf16x3: the towers' GEMMs (patch embedding, every encoder GEMM) as split-operand bf16 products
         self._rt.x3 = precision == "bf16x3"
         if freeze_clip:
