@@ -34,6 +34,16 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("t_fc2_dgrad", RT, 2048, 512, True, False, torch.bfloat16, _lib.EPI_DQGELU, 1),
     ("t_fc1_dgrad", RT, 512, 2048, True, False, torch.bfloat16, 0, 1),
     ("t_qkv_dgrad", RT, 512, 1536, True, False, torch.bfloat16, 0, 1),
+    # the bf16 mode's fp32 residual stream (round 5): out-projection and fc2 write the fp32 sum
+    ("fc2_fwd_r32", R, 768, 3072, True, True, torch.float32, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    ("out_fwd_r32", R, 768, 768, True, True, torch.float32, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    ("t_fc2_fwd_r32", RT, 512, 2048, True, True, torch.float32, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    ("t_out_fwd_r32", RT, 512, 512, True, True, torch.float32, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
+    ("t_out_dgrad", RT, 512, 512, True, False, torch.bfloat16, 0, 1),
+    ("t_fc1_wgrad", 2048, 512, RT, False, False, torch.float32, _lib.EPI_BETA, 2),
+    ("t_fc2_wgrad", 512, 2048, RT, False, False, torch.float32, _lib.EPI_BETA, 2),
+    ("t_qkv_wgrad", 1536, 512, RT, False, False, torch.float32, _lib.EPI_BETA, 2),
+    ("t_out_wgrad", 512, 512, RT, False, False, torch.float32, _lib.EPI_BETA, 2),
     # the same shapes with K = 64: prologue + epilogue cost per tile
     ("fc1_k64", R, 3072, 64, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("qkv_k64", R, 2304, 64, True, True, torch.bfloat16, _lib.EPI_BIAS, 1),
@@ -112,7 +122,7 @@ for name, M, N, Kd, akm, bkm, odt, flags, split in SHAPES:
     if split == 0:
         continue
     ws = torch.empty(split * M * (N + 1), device="cuda") if split > 1 else None  # slabs + bias partials
-    bg = torch.zeros(M, device="cuda") if odt == torch.float32 else None
+    bg = torch.zeros(M, device="cuda") if (odt == torch.float32 and not akm and not bkm) else None  # wgrad only
     kw = dict(bias=bias if flags & _lib.EPI_BIAS else None, residual=res, ldr=N, aux=aux, ldaux=N, flags=flags,
               split_k=split, workspace=ws, bias_grad=bg)
     if os.environ.get("GEMM_TORCH"):  # hipBLASLt via torch.matmul, plain product, for comparison

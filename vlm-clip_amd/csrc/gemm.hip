@@ -1535,6 +1535,13 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     p.c_scale = d->c_scale;
     p.raster = raster_rows(true);
     p.var = d->force_small_tile;  // 40: the 8-wave fp8 kernel (A/B of the persistent 4-wave one)
+    {
+      static const int env = [] {  // CLIPMI_FP8_VAR=40 / 41: every fp8 product on the 8-wave / 4-wave kernel (A/B)
+        const char* e = getenv("CLIPMI_FP8_VAR");
+        return e ? atoi(e) : 0;
+      }();
+      if (p.var == 0 && (env == 40 || env == 41)) p.var = env;
+    }
     p.vec = (d->ldc % 4 == 0) && (d->ldr % 4 == 0) && (d->ldaux % 4 == 0) && ((uintptr_t)d->C % 16 == 0) &&
             ((uintptr_t)d->residual % 16 == 0) && ((uintptr_t)d->aux % 16 == 0);
     p.vec8 = d->c_dtype == CLIPMI_BF16 && d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldr % 8 == 0 && d->ldaux % 8 == 0 &&

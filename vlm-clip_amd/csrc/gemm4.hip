@@ -1037,13 +1037,12 @@ const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags) {
 // beta epilogue (one split), with the fused bias gradient when bg != nullptr
 // MXFP8 forward products on the persistent 4-wave kernel: K % 256 == 0 (whole scale pairs) and at
 // least one full tile; nullptr leaves them to gemm.hip's 8-wave fp8 kernel
-// Production: long-K products (fc2, K = 4096: 1.48 vs 1.87 ms at L/14@336 B = 512) and bias-only
-// outputs (qkv: 1.41 vs 1.50 ms); the residual / activation epilogues at K = 1024 measured equal or
-// 5 % slower than the 8-wave kernel (its non-persistent workgroups spread the epilogue stores over
-// time; profiles/r04_fp8_gemm.log).  41: this kernel for every covered shape (tests, A/B).
+// Production: every covered shape (round 5).  Round 4 kept the residual / activation epilogues at K = 1024
+// (fc1 -> MXFP8, out-proj) on the 8-wave kernel, equal or 5 % slower here in isolation
+// (profiles/r04_fp8_gemm.log); in config 5's step this kernel for all of them measured equal throughput
+// and a 3.5 % shorter mean fp8 launch (profiles/r05_cfg5_fp8_kernel_ab.log).  40: the 8-wave kernel (A/B).
 const char* dispatch_w4_fp8(const GemmP& p, hipStream_t s, bool f32o, bool q8o, int flags) {
   if (p.K % W8_PAIR != 0 || p.M < BT || p.N < BT || p.var == 40) return nullptr;  // 40: the 8-wave kernel (A/B)
-  if (p.var != 41 && !(p.K >= 2048 || (flags == CLIPMI_EPI_BIAS && !q8o && !f32o))) return nullptr;
   constexpr int B8 = CLIPMI_EPI_BIAS, Q8 = CLIPMI_EPI_QGELU, R8 = CLIPMI_EPI_RESID;
   if (q8o) {
     if (flags != (B8 | Q8)) return nullptr;

@@ -12,6 +12,7 @@
 #include "common.h"
 #include "internal.h"
 #include <cstring>
+#include <type_traits>
 
 namespace {
 
@@ -160,7 +161,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
   // reduction (as ln_fwd_kernel).  Two rows for D <= 512 (text: 67 -> 65 us at R = 78,848); one for
   // wider rows, where two rows' registers (164 VGPRs at D = 768) cost a wave per SIMD and measured
   // 3-4 % slower (tools/ln_bench.py, profiles/r02_ln_bwd_ab.log)
-  constexpr int RPW = NP * PS <= 8 ? 2 : 1;
+  // fp32 x with bf16 gradients (the fp32 residual stream): two rows at D = 768 too, 285 vs 293 us at
+  // R = 201,728 (profiles/r05_ln_rows_per_wave_ab.log; with bf16 x two rows measured 234 vs 223 us)
+  constexpr bool MIXED = std::is_same<TX, float>::value && !std::is_same<T, float>::value;
+  constexpr int RPW = (NP * PS <= 8 || MIXED) ? 2 : 1;
   for (int row0 = (blockIdx.x * 4 + wave) * RPW; row0 < R; row0 += gridDim.x * 4 * RPW) {
     float g[RPW][NP][PS], xh[RPW][NP][PS], rr[RPW][NP][PS], d[RPW][NP][PS];
     float mu[RPW], rs[RPW];
