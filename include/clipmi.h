@@ -10,13 +10,12 @@
  * The reference has no native boundary: its hot path is PyTorch/HF
  * module calls.  Each entry point below names the reference op it replaces.
  *
- * Collectives are not in this ABI.  SURVEY.md §8b sketched clipmi_ctx / clipmi_workspace_size /
- * clipmi_allgather_embed / clipmi_reducescatter_grad / clipmi_allreduce_grads; the build keeps the
- * host side PyTorch-ROCm as north_star allows, so the data-parallel exchanges (all-gather of the
- * normalised features, reduce-scatter of their gradients, the bucketed gradient all-reduce) are
- * issued through torch.distributed (backend "nccl" = RCCL over xGMI) by clipmi/towers.py
- * (ContrastiveFn) and clipmi/trainer.py (GradBucketReducer), on the same HIP streams these entry
- * points run on.  Workspaces are sized per call by the *_ws() queries (no context object).
+ * Collectives: clipmi_allgather_embed / clipmi_reducescatter_grad /
+ * clipmi_allreduce_grads below run the data-parallel exchanges over RCCL for FFI hosts with one process
+ * per GPU (communicator from clipmi_comm_unique_id + clipmi_comm_init).  The PyTorch host issues the same
+ * exchanges through torch.distributed (backend "nccl" = RCCL over xGMI) in clipmi/towers.py (ContrastiveFn)
+ * and clipmi/trainer.py (GradBucketReducer), on the same HIP streams these entry points run on.
+ * Workspaces are sized per call by the *_ws() queries (no context object).
  */
 #ifndef CLIPMI_H
 #define CLIPMI_H
@@ -377,6 +376,23 @@ int clipmi_prof_disarm(void);
  * their event-bracketed durations are not the kernel's own. */
 int clipmi_prof_stream(void* stream);
 int clipmi_prof_read(int max, float* ms, double* flops);
+
+/* ---- Data-parallel collectives over RCCL --------------------------------------------
+ * One communicator per process / GPU.  Rank 0 creates the 128-byte id, the host distributes it (any channel)
+ * and every rank calls clipmi_comm_init with it; librccl is opened on first use (CLIPMI_ERR_UNSUPPORTED when
+ * it is absent).  All enqueue on `stream`; counts are elements.
+ *   allgather_embed     global[r * count + i] = local_r[i]  (the L2-normalised [B, E] features of every rank
+ *                       before the [B, Bg] similarities; model_m.py:146-171 on one device)   dtype f32 / bf16
+ *   reducescatter_grad  local_r[i] = sum_s global_s[r * count + i]  (the column-direction feature gradients back
+ *                       to their owners)
+ *   allreduce_grads     grads[i] = sum_s grads_s[i], in place, fp32  (a bucket of the gradient arena: the
+ *                       data-parallel sum of trainer.py:92's loss.backward) */
+int clipmi_comm_unique_id(void* id /* 128 bytes */);
+int clipmi_comm_init(void** comm, const void* id, int nranks, int rank);
+int clipmi_comm_destroy(void* comm);
+int clipmi_allgather_embed(void* stream, void* comm, int dtype, const void* local, void* global, int64_t count);
+int clipmi_reducescatter_grad(void* stream, void* comm, int dtype, const void* global, void* local, int64_t count);
+int clipmi_allreduce_grads(void* stream, void* comm, float* grads, int64_t count);
 
 #ifdef __cplusplus
 }

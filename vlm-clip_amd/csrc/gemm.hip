@@ -1597,10 +1597,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.dbg = gemm_stamp_buffer();
   p.stagger = 0;
   p.first_round = num_cus();
-  if (d->force_small_tile >= 200 && d->force_small_tile < 300) {  // A/B hook: 2xx the persistent 4-wave kernel,
-    p.var = 28;                                                    // half its workgroups starting xx s_sleeps late
-    p.stagger = d->force_small_tile % 100;
-  } else if (d->force_small_tile >= 100 && d->force_small_tile < 200) {  // 1xx the 8-wave kernel, first-round stagger xx
+  if (d->force_small_tile >= 100 && d->force_small_tile < 200) {  // 1xx the 8-wave kernel, first-round stagger xx
     p.var = 9;
     p.stagger = d->force_small_tile % 100;
   } else if (d->force_small_tile >= 2) p.var = d->force_small_tile;

@@ -569,11 +569,6 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_w4p_kernel(GemmP p, float* bia
     w4_stage_dma<AK, BKM>(smem, p, w, wave, m0, n0, kbeg, kend, ns > 0);
     w4_stage_dma<AK, BKM>(smem + W4_STAGE, p, w, wave, m0, n0, kbeg + 64, kend, ns > 1);
   };
-  // A/B hook (force_small_tile 2xx): half of every XCD's workgroups start p.stagger s_sleep(127)s late, so
-  // with equal items per workgroup the two halves' epilogues stay offset for the whole launch
-  if (p.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   if (item < nitems) prologue_dma(item);
   // a deferred reduction (the previous weight gradient's split-K sum or LayerNorm affine sum) while the
   // first stages land
