@@ -1642,6 +1642,11 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
       GemmP q = p;
       q.tiles_n = (d->N + BT - 1) / BT;
       q.ntiles = q.tiles_n * ((d->M + BT - 1) / BT);
+      // weight gradients with more column than row tiles (fc2: M = 768, N = 3072) walk each k-slab's
+      // tiles column-major, so the ~32 items an XCD holds at once share the few row panels instead of
+      // spanning every column panel (L2 fetch modelled 1.66x -> 1.25x of the compulsory panels,
+      // tools/gemm_l2_model.py); CLIPMI_RASTER overrides
+      if (wlayout && !getenv("CLIPMI_RASTER") && q.tiles_n > q.ntiles / q.tiles_n) q.raster = q.ntiles / q.tiles_n;
       label = dispatch256(q, splits, s, f32o, sel, d->flags, d->bias_grad);
     }
     if (!label) {
