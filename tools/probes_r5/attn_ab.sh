@@ -1,0 +1,8 @@
+# A/B of the attention kernels between the tree's library and an alt build (clipmi/alt/libclipmi_$1.so), A B A B
+set -e
+R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
+ALT=$R/vlm-clip_amd/clipmi/alt/libclipmi_$1.so; shift
+for r in A B A B; do
+  echo "== $r"
+  if [ $r = A ]; then timeout -k 10 120 python3 tools/attn_bench.py "$@"; else CLIPMI_LIB=$ALT timeout -k 10 120 python3 tools/attn_bench.py "$@"; fi
+done

@@ -846,19 +846,23 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
       }
     }
   };
-  auto load_meta = [&](int item, float& l2v, int& kov) {
+  // the raw loaded values stay untouched until store_meta: arithmetic on them right after the loads
+  // made the compiler wait (vmcnt(0)) there -- for them and for the next item's K/V fragment loads
+  // issued just before -- in the middle of the phase-A -> phase-B handover (ViT-B/16 backward
+  // 952 -> 933 us, profiles/r05_attn_bwd_meta_ab.log)
+  auto load_meta = [&](int item, float& lse_raw, int64_t& km_raw) {
     const int b = item / H, h = item - b * H;
-    l2v = __builtin_huge_valf();
-    kov = 0;
+    lse_raw = __builtin_huge_valf();
+    km_raw = 0;
     if (t < N) {
-      l2v = p.lse[((int64_t)b * H + h) * N + t] * LOG2E;
-      kov = !p.kmask || p.kmask[(int64_t)b * N + t] != 0;
+      lse_raw = p.lse[((int64_t)b * H + h) * N + t];
+      km_raw = p.kmask ? p.kmask[(int64_t)b * N + t] : 1;
     }
   };
-  auto store_meta = [&](int sl, float l2v, int kov) {
+  auto store_meta = [&](int sl, float lse_raw, int64_t km_raw) {
     if (t < NPAD) {
-      arr[sl * 3 * NPAD + t] = l2v;
-      ((int*)arr)[sl * 3 * NPAD + 2 * NPAD + t] = kov;
+      arr[sl * 3 * NPAD + t] = lse_raw * LOG2E;
+      ((int*)arr)[sl * 3 * NPAD + 2 * NPAD + t] = km_raw != 0;
     }
   };
 
@@ -866,7 +870,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
   bf16x8 kf[NBA][2], vf[NBA][2];
   {
     float l2v;
-    int kov;
+    int64_t kov;
     load_kvfrag(item, kf, vf);
     load_meta(item, l2v, kov);
     issue_qdo(item);
@@ -926,7 +930,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     // ---- phase B: dQ (K image, V image)
     const bool more = nxt < nitems;
     float l2n = 0.f;
-    int kon = 0;
+    int64_t kon = 0;
     if (more) {
       load_kvfrag(nxt, kf, vf);
       load_meta(nxt, l2n, kon);
