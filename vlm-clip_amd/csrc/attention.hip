@@ -1367,9 +1367,79 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
     const char* Vimg = Kimg + FA_TILE / 2;
     const int k0 = kt * FA_KT;
     const int nsteps = min(2, (N - k0 + 31) >> 5);  // 32-key steps holding valid keys
-    // Unmasked (vision): the block loop is straight-line code -- every block computed (rows past N
-    // read zero-filled Q), every 32-key step computed (keys past N get P = 0), the offset moved
-    // per lane by select -- so the compiler interleaves one block's MFMAs with another's softmax.
+    if constexpr (!MASKED) {
+      // Unmasked (vision): straight-line code -- every block computed (rows past N read zero-filled Q),
+      // every 32-key step computed (keys past N get P = 0).  The tile's K fragments are read from LDS
+      // once and serve every query block, and the P.V products run V-fragment-outer over the blocks'
+      // packed P, so each V fragment is read once too: the per-block form re-read both for every block
+      // (the compiler cannot merge loads across the rescale branch's ballot) -- 4x the LDS fragment
+      // traffic of 8 waves per CU, which co-bounded the tile with the MFMAs.  Same MFMAs, operands and
+      // accumulation order per output: bitwise the per-block form's results.
+      bf16x8 kfr[4][2];
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) kfr[st][kk] = frag_row(Kimg, st * 16 + li, kk * 4 + g);
+      const bool tail = k0 + FA_KT > N;  // wave-uniform: only the last tile holds keys past N
+      bf16x8 pfu[QPW][2];
+#pragma unroll
+      for (int u = 0; u < QPW; ++u) {
+        f32x4 sc[4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          sc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            sc[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfr[st][kk], qf[u][kk], sc[st], 0, 0, 0);
+        }
+        float mt = NEG_INF;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          if (tail) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (k0 + st * 16 + 4 * g + r >= N) sc[st][r] = NEG_INF;
+          }
+          mt = fmaxf(mt, fmaxf(fmaxf(sc[st][0], sc[st][1]), fmaxf(sc[st][2], sc[st][3])));
+        }
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float mt2 = mt * c2;
+        // deferred maximum: move the offset only when this tile's max exceeds it by > FA_THR; the rescale
+        // only when some row of the wave moved its offset (wave-uniform branch, untaken on most tiles)
+        const float mn = mt2 > m[u] + FA_THR ? fmaxf(m[u], mt2) : m[u];
+        if (__builtin_amdgcn_read_exec() && __any(mn != m[u])) {
+          const float f = __builtin_amdgcn_exp2f(m[u] - mn);  // 1 unmoved, 0 on the first tile
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+        }
+        m[u] = mn;
+        const float off = m[u] == NEG_INF ? 0.f : m[u];
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[st][r] = __builtin_amdgcn_exp2f(fmaf(sc[st][r], c2, -off));
+        pfu[u][0] = pack8(sc[0], sc[1]);
+        pfu[u][1] = pack8(sc[2], sc[3]);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int u = 0; u < QPW; ++u) accl[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pfu[u][ks], accl[u], 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const bf16x8 vt = frag_tr(Vimg, ks * 32, v * 16, lane);
+#pragma unroll
+          for (int u = 0; u < QPW; ++u)
+            acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pfu[u][ks], acc[u][v], 0, 0, 0);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < QPW; ++u) {
       if constexpr (MASKED) {
