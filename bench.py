@@ -107,7 +107,7 @@ PEAKS = {"gemm_fp8": PEAK_FP8_TFLOPS, "gemm_f32": PEAK_FP32_TFLOPS}
 # explicitly so the file read is the one committed for this build, not the newest on disk
 TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r05_traffic_fwd_dgrad.json",
                  "gemm256_wgrad": "profiles/r05_traffic_wgrad.json",
-                 "attention": "profiles/r02_traffic_attention.json"}
+                 "attention": "profiles/r05_traffic_attention.json"}
 
 
 def vision_gemm_shapes(cfg, B, train, resid32=False):
