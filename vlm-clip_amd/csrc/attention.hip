@@ -1396,37 +1396,49 @@ __global__ __launch_bounds__(FA_W * 64, 2) void attn_fwd_fa(AttnP p, int causal,
           for (int kk = 0; kk < 2; ++kk)
             sc[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfr[st][kk], qf[u][kk], sc[st], 0, 0, 0);
         }
-        float mt = NEG_INF;
+        if (tail) {
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          if (tail) {
+          for (int st = 0; st < 4; ++st)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (k0 + st * 16 + 4 * g + r >= N) sc[st][r] = NEG_INF;
-          }
+        }
+        // the exponent arguments relative to the current offset first, and the tile's max taken over them:
+        // fmaf's results are canonical floats, so the max needs no v_max canonicalisation per MFMA output
+        // (64 VALU instructions per tile; the softmax is VALU-issue bound beside the MFMAs)
+        const bool first = m[u] == NEG_INF;
+        const float off = first ? 0.f : m[u];
+        float mt = NEG_INF;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[st][r] = fmaf(sc[st][r], c2, -off);
           mt = fmaxf(mt, fmaxf(fmaxf(sc[st][0], sc[st][1]), fmaxf(sc[st][2], sc[st][3])));
         }
         mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
         mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        const float mt2 = mt * c2;
-        // deferred maximum: move the offset only when this tile's max exceeds it by > FA_THR; the rescale
-        // only when some row of the wave moved its offset (wave-uniform branch, untaken on most tiles)
-        const float mn = mt2 > m[u] + FA_THR ? fmaxf(m[u], mt2) : m[u];
-        if (__builtin_amdgcn_read_exec() && __any(mn != m[u])) {
-          const float f = __builtin_amdgcn_exp2f(m[u] - mn);  // 1 unmoved, 0 on the first tile
+        // deferred maximum: move the offset (by d) only on the first tile or when this tile's max exceeds it
+        // by > FA_THR; the rescale only when some row of the wave moved (wave-uniform branch, untaken on
+        // most tiles)
+        const float d = (first || mt > FA_THR) ? mt : 0.f;
+        if (__builtin_amdgcn_read_exec() && __any(d != 0.f)) {
+          const float f = first ? 0.f : __builtin_amdgcn_exp2f(-d);
 #pragma unroll
           for (int v = 0; v < 4; ++v)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[u][v][r] *= f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) accl[u][r] *= f;
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[st][r] -= d;
         }
-        m[u] = mn;
-        const float off = m[u] == NEG_INF ? 0.f : m[u];
+        m[u] = off + d;
 #pragma unroll
         for (int st = 0; st < 4; ++st)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) sc[st][r] = __builtin_amdgcn_exp2f(fmaf(sc[st][r], c2, -off));
+          for (int r = 0; r < 4; ++r) sc[st][r] = __builtin_amdgcn_exp2f(sc[st][r]);
         pfu[u][0] = pack8(sc[0], sc[1]);
         pfu[u][1] = pack8(sc[2], sc[3]);
       }
