@@ -657,7 +657,15 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
       const f32x4 d4 = *LDS_PTR(const f32x4, c.delta + q0);
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
+        // non-causal: the key mask and -delta ride in the accumulators' initial values (a masked key's
+        // scores start at -inf, so exp2 gives P = 0; dP starts at -delta): no select and no subtract per
+        // element -- the phases are VALU-issue bound beside their MFMAs
         f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+        if constexpr (!CAUSAL) {
+          const float s0 = kok[u] ? 0.f : NEG_INF;
+          sc = f32x4{s0, s0, s0, s0};
+          dp = f32x4{-d4[0], -d4[1], -d4[2], -d4[3]};
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kf[u][kk], sc, 0, 0, 0);
@@ -665,10 +673,16 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool ok = kok[u] && (!CAUSAL || key[u] <= q0 + r);
-          const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l4[r]) : 0.f;
-          pt[u][tau][r] = pv;
-          ds[u][tau][r] = pv * (dp[r] - d4[r]);
+          if constexpr (!CAUSAL) {
+            const float pv = __builtin_amdgcn_exp2f(sc[r] * c.c2 - l4[r]);
+            pt[u][tau][r] = pv;
+            ds[u][tau][r] = pv * dp[r];
+          } else {
+            const bool ok = kok[u] && key[u] <= q0 + r;
+            const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l4[r]) : 0.f;
+            pt[u][tau][r] = pv;
+            ds[u][tau][r] = pv * (dp[r] - d4[r]);
+          }
         }
       }
       if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);  // one tau's operands live at a time
@@ -739,9 +753,14 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
       }
       const int k0 = ks * 32 + tau * 16 + 4 * g;
       const i32x4 ko = *LDS_PTR(const i32x4, c.keyok + k0);
+      // non-causal: key mask and -delta as the accumulators' initial values (see bwd_phase_a)
+      f32x4 seed = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (!CAUSAL) seed = f32x4{ko[0] ? 0.f : NEG_INF, ko[1] ? 0.f : NEG_INF, ko[2] ? 0.f : NEG_INF,
+                                          ko[3] ? 0.f : NEG_INF};
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+        f32x4 sc = seed, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!CAUSAL) dp = f32x4{-dl[u], -dl[u], -dl[u], -dl[u]};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[kk], qf[u][kk], sc, 0, 0, 0);
@@ -749,9 +768,13 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool ok = ko[r] && (!CAUSAL || k0 + r <= q[u]);
-          const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l2[u]) : 0.f;
-          ds[u][tau][r] = pv * (dp[r] - dl[u]);
+          if constexpr (!CAUSAL) {
+            ds[u][tau][r] = __builtin_amdgcn_exp2f(sc[r] * c.c2 - l2[u]) * dp[r];
+          } else {
+            const bool ok = ko[r] && k0 + r <= q[u];
+            const float pv = ok ? __builtin_amdgcn_exp2f(sc[r] * c.c2 - l2[u]) : 0.f;
+            ds[u][tau][r] = pv * (dp[r] - dl[u]);
+          }
         }
       }
       if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
