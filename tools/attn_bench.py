@@ -9,7 +9,7 @@ from clipmi import kernels as K, towers as T
 SHAPES = [("vision_b16", 1024, 197, 12, False), ("text", 1024, 77, 8, True), ("vision_l14", 512, 257, 16, False),
           ("vision_l14_336", 256, 577, 16, False)]
 only = sys.argv[1:] or None
-NWS = os.environ.get("ATTN_NWS", "16").split(",")  # whole-K/V kernels: waves per workgroup (A/B in one process)
+NWS = os.environ.get("ATTN_NWS", "8").split(",")  # whole-K/V kernels: waves per workgroup (8 = production; A/B in one process)
 
 
 def timeit(f, n=10):
