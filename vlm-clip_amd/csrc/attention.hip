@@ -609,17 +609,6 @@ __device__ __forceinline__ void raw_barrier_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// s_waitcnt vmcnt(n), n in {0, 4, 8, 16} (wave-uniform): every VMEM operation but the wave's n youngest
-// retired.  attn_bwd_pf's phase A ends in its output stores (dK / dV: 8 global_store_dwordx2 per key
-// block; a block below nkb always has a row < N, so its stores issue); the K / V image DMAs the barrier
-// after it waits for came before them, so the stores may stay in flight.
-__device__ __forceinline__ void wait_vm_but(int n) {
-  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 
 // Per-item context of the prefetching backward's two phases.
 struct BwdCtx {
@@ -914,8 +903,6 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     issue_qdo(item);
     store_meta(0, l2v, kov);
   }
-  // phase A's output stores stay in flight across the barrier after it (wait_vm_but)
-  const int nst_a = NBM == 2 ? 8 * ((wave < nkb) + (wave + NW < nkb)) : 0;
   for (int it = 0;; ++it) {
     const int sl = it & 1;
     const float* lse2 = arr + sl * 3 * NPAD;
@@ -924,14 +911,6 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
     ATT_ST(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // Q/dO/O(i), meta(i) ready; K/V images free
-    // The K / V fragments (loaded in the previous item's phase B, landed by the wait above) as fresh
-    // values: left as loop-carried load results, the compiler's merged wait for them (vmcnt(0)) sat at
-    // phase A's first MFMA -- behind the K / V image DMAs issued below, so those never overlapped
-    // phase A -- and another before the next item's fragment loads reuse their registers.
-#pragma unroll
-    for (int u = 0; u < NBA; ++u)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) asm volatile("" : "+v"(kf[u][kk]), "+v"(vf[u][kk]));
     ATT_ST(1);
     const int cur = item, nxt = item + gridDim.x;
     const int b = cur / H, h = cur - b * H;
@@ -971,7 +950,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_pf(AttnP p, int nitems) {
       }
     }
     ATT_ST(3);
-    wait_vm_but(nst_a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // K/V(i) images landed; phase A's reads of Q/dO done
     ATT_ST(4);
 
