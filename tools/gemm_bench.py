@@ -10,6 +10,8 @@ from clipmi import kernels as K, _lib
 
 R = 1024 * 197
 RT = 1024 * 77
+if os.environ.get("GEMM_ROWS"):  # GEMM_ROWS=vision,text: other batches (config 2, B/32 B=256: 12800,19712)
+    R, RT = (int(x) for x in os.environ["GEMM_ROWS"].split(","))
 SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor, out dtype, flags, split
     ("fc1_fwd", R, 3072, 768, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_PRE, 1),
     ("fc2_fwd", R, 768, 3072, True, True, torch.bfloat16, _lib.EPI_BIAS | _lib.EPI_RESID, 1),
