@@ -26,6 +26,8 @@ def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo"):
     import sys
     if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
         os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
+    if world == 1:  # one-rank group: take the collective branches anyway (each is the identity)
+        os.environ["CLIPMI_DP_FORCE_COLLECTIVES"] = "1"
     sys.path.insert(0, os.path.join(REPO, "vlm-clip_amd"))
     import torch.distributed as dist
     from clipmi import CLIPWithAdapters, synth
@@ -110,3 +112,39 @@ def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared, ba
             scale = max(float(np.abs(r).max()), 1e-2 * gmax)
             worst = max(worst, (float(np.abs(g[n] - r).max()) / scale, n))
         assert worst[0] < 1e-4, worst
+
+
+@pytest.mark.parametrize("overlap,chunk", [(True, None), (False, 3)])
+def test_one_rank_rccl_group_matches_single_device(overlap, chunk):
+    """The RCCL (backend nccl) branches of the data-parallel path -- the embedding all-gather and
+    gradient reduce-scatter around the contrastive loss, the bucketed all-reduce from the comm stream
+    (overlap) or after the backward -- executed where only one GPU is visible: a one-rank group with
+    CLIPMI_DP_FORCE_COLLECTIVES=1 takes every collective branch, each then the identity, so the result
+    must equal the group-free run on the same 4 samples."""
+    import torch.multiprocessing as mp
+    from clipmi import CLIPWithAdapters, synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30300 + os.getpid() % 500 + 37 * int(overlap)
+    p = ctx.Process(target=_worker, args=(0, 1, port, q, overlap, chunk, False, "nccl"))
+    p.start()
+    r = q.get(timeout=200)
+    if r[1] is None:
+        p.kill()
+        raise AssertionError(f"rank 0 failed:\n{r[2]}")
+    p.join(120)
+    m = CLIPWithAdapters("tiny", use_shared_adapters=False, freeze_clip=False, device="cuda:0", precision="fp32",
+                         pooling="eos")
+    b = {k: torch.from_numpy(v).cuda() for k, v in synth.synthetic_batch(m.config, 4, seed=5).items()}
+    out = m(**b)
+    out["loss"].backward()
+    torch.cuda.synchronize()
+    ref = {n: q_.grad.detach().cpu().numpy() for n, q_ in m.named_parameters() if q_.grad is not None}
+    gmax = max(float(np.abs(v).max()) for v in ref.values())
+    _, loss, g = r
+    assert abs(loss - out["loss"].item()) < 1e-5, (loss, out["loss"].item())
+    worst = (0.0, "")
+    for n, v in ref.items():
+        scale = max(float(np.abs(v).max()), 1e-2 * gmax)
+        worst = max(worst, (float(np.abs(g[n] - v).max()) / scale, n))
+    assert worst[0] < 1e-4, worst

@@ -713,9 +713,16 @@ def _rccl(group):
     return dist.get_backend(group) == "nccl"
 
 
+def force_collectives():
+    """CLIPMI_DP_FORCE_COLLECTIVES=1 (tests only): a one-rank group still takes the collective branches
+    (all-gather, reduce-scatter, bucketed all-reduce), each then the identity, so a one-GPU box runs
+    the RCCL code paths (tests/test_gpu_dp.py)."""
+    return os.environ.get("CLIPMI_DP_FORCE_COLLECTIVES") == "1"
+
+
 def _gather(x, group, world):
     """All-gather rows over the group (RCCL all_gather_into_tensor; list form for gloo)."""
-    if world == 1:
+    if world == 1 and not (group is not None and force_collectives()):
         return x
     x = x.contiguous()
     if _rccl(group):
@@ -730,7 +737,7 @@ def _gather(x, group, world):
 def _reduce_scatter(x, group, world):
     """Sum over the group, keep this rank's row block (RCCL reduce_scatter_tensor; gloo:
     all_reduce + slice, which gloo supports for device tensors)."""
-    if world == 1:
+    if world == 1 and not (group is not None and force_collectives()):
         return x
     x = x.contiguous()
     n = x.shape[0] // world

@@ -130,7 +130,7 @@ class FusedAdamW:
         self._gn = (ctypes.c_int64 * n)()
         self._norm_ws = torch.empty(int(_lib.lib().clipmi_grad_norm_multi_ws(n)), dtype=torch.uint8, device=dev)
         self.reducer = None
-        if process_group is not None and dist.get_world_size(process_group) > 1:
+        if process_group is not None and (dist.get_world_size(process_group) > 1 or T.force_collectives()):
             self.reducer = GradBucketReducer(self.arenas, process_group)
 
     def overlap_with(self, model):
