@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=32,
                     help="pairs per CPU-baseline step (SURVEY 8d: B = 32; 0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--parity-steps", type=int, default=5,
+                    help="N=1, bf16 full fine-tune: also time this many steps of the bf16x3 mode (the mode that meets "
+                         "north_star's 1e-3 logits) in the same run, reported under `parity_mode` (0 = skip)")
+    ap.add_argument("--parity-warmup", type=int, default=2)
     ap.add_argument("--launch-check", action="store_true",
                     help="test hook: each rank prints its rank/world and exits before touching the GPU")
     return ap.parse_args()
@@ -296,6 +300,48 @@ def family_roofline(name, launches, cfg, B, train, resid32=False, x3=False):
     return res
 
 
+def parity_mode_run(args, cfg, dev, batch):
+    """The bf16x3 mode (fp32 activations, every tower GEMM a bf16x3 split product: max |dlogit| 1.1e-4 against
+    the fp32 reference at this config, profiles/r05_config3_full_size_parity.log; test bound 1e-3) timed on the
+    same workload and batch as the headline, after it, with the same step (fwd + bwd + clip + AdamW)."""
+    from clipmi import CLIPWithAdapters
+    from clipmi.trainer import FusedAdamW, linear_schedule_with_warmup
+    model = CLIPWithAdapters(args.model, use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                             freeze_clip=False, device=dev, precision="bf16x3", fast_init=True)
+    params = [p for n, p in model.named_parameters() if p.requires_grad]
+    opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas())
+    total = args.parity_warmup + args.parity_steps
+
+    def step(i):
+        out = model(**batch)
+        opt.zero_grad()
+        opt.armed_backward(out["loss"])
+        opt.clip_grad_norm(1.0)
+        opt.step(lr=5e-5 * linear_schedule_with_warmup(i, 0, total))
+        return out["loss"]
+
+    for i in range(args.parity_warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.parity_warmup, total):
+        loss = step(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    value = args.batch * args.parity_steps / el
+    step_flops_pair = 3 * C.forward_flops_per_pair(cfg)
+    log(f"parity mode (bf16x3): {args.parity_steps} steps in {el:.3f} s = {value:.1f} pairs/s")
+    res = {"precision": "bf16x3", "value": round(value, 2), "unit": "pairs/s",
+           "ms_per_step": round(el / args.parity_steps * 1e3, 2), "steps": args.parity_steps,
+           "warmup": args.parity_warmup, "loss": round(float(loss.item()), 4), "max_dlogit_bound": 1e-3,
+           "dtype": "fp32 (tower GEMMs and attention products as bf16x3 split products, fp32 accumulation)",
+           # three bf16 MFMA products per fp32 one: priced against a third of the bf16 peak
+           "mfma_frac_step": round(value * step_flops_pair / (PEAK_BF16_TFLOPS / 3 * 1e12), 4)}
+    del model, opt, params
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -440,6 +486,10 @@ def main():
         "rooflines": {k: v for k, v in roofs.items() if k != main_fam},
         "cpu_baseline": None,
     }
+    if (world == 1 and args.parity_steps > 0 and args.precision == "bf16" and not adapters):
+        del model, opt, params
+        torch.cuda.empty_cache()
+        result["parity_mode"] = parity_mode_run(args, cfg, dev, batch)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, args.cpu_steps, adapters)
     if rank == 0:

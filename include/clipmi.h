@@ -146,6 +146,12 @@ int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const void* dy, 
                           int64_t ldx, const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx,
                           const void* dres, int64_t ldres, float* dw, float* db, int beta_wb, void* ws,
                           int64_t ws_bytes, int R, int D);
+/* the same with the affine weight's dtype given: w_dtype = dtype, or CLIPMI_F32 with fp32 x (the vision
+   pre_layrnorm on the fp32 residual stream normalises with the fp32 master weights in its forward) */
+int clipmi_layernorm_bwd3(void* stream, int x_dtype, int dtype, int w_dtype, const void* dy, int64_t lddy,
+                          const void* x, int64_t ldx, const float* mean, const float* rstd, const void* w, void* dx,
+                          int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db, int beta_wb, void* ws,
+                          int64_t ws_bytes, int R, int D);
 /* out[n] (+)= sum_r x[r][n]  (bias gradients of every Linear on the path) */
 int64_t clipmi_colsum_ws(int R, int N);
 int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, int N, float* out, int beta, void* ws,
@@ -224,6 +230,14 @@ int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t* o8, uint8
                                const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, const void* o, const float* lse, const void* dout,
                          void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
+/* The bf16x3 precision mode's attention (csrc/attention_x3.hip): fp32 operands and outputs exactly as
+   clipmi_attention_fwd / _bwd with dtype CLIPMI_F32, every product (q k^T, P v, dO v^T, dS k, dS^T q, P^T dO)
+   run as three bf16 MFMA products of the hi / lo operand splits (~2^-16 relative per product).  N > 288 falls
+   back to the exact-f32 kernels. */
+int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, float* lse, const int64_t* attention_mask,
+                            int causal, int B, int H, int N, int D);
+int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void* o, const float* lse, const void* dout,
+                            void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 
 /* ---- Encoder engine: whole CLIPEncoder fwd/bwd in one call ([HF] :477-482, :362-383) ---------- */
 typedef struct clipmi_layer_w { /* activation dtype; qkv_w = [q;k;v] rows, [3D, D] */

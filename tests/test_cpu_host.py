@@ -91,8 +91,9 @@ def test_epilogue_flag_without_operand_is_rejected(flag, operand):
 
 @pytest.mark.parametrize("case", ["D", "A", "ln_w", "saved", "ws"])
 def test_adapter_bad_arguments_rejected(case):
-    """clipmi_adapter_fwd / _bwd reject D or A not a multiple of 8, ln without its weights, a
-    missing activation buffer (act carries the bottleneck between the launches) and a short backward
+    """clipmi_adapter_fwd / _bwd reject D or A not a multiple of 8 in bf16 (16-byte MFMA rows; fp32 takes any
+    width, as nn.Linear does: test_gpu_kernels.test_adapter_fused_pooled_rows_matches_torch), ln without its
+    weights, a missing activation buffer (act carries the bottleneck between the launches) and a short backward
     workspace with CLIPMI_ERR_INVALID before any launch (pointers here are never dereferenced)."""
     from clipmi import _lib
     from clipmi import towers as T  # noqa: F401  (declares the prototypes)
@@ -111,7 +112,8 @@ def test_adapter_bad_arguments_rejected(case):
             A = 60
         lnw = None if case == "ln_w" else p
         act = None if case == "saved" else p
-        st = L.clipmi_adapter_fwd(None, 0, R, D, A, p, D, p, p, p, p, lnw, p, 1e-5, 1, p, D, p, act, p, p, p)
+        dt = _lib.BF16 if case in ("D", "A") else _lib.F32
+        st = L.clipmi_adapter_fwd(None, dt, R, D, A, p, D, p, p, p, p, lnw, p, 1e-5, 1, p, D, p, act, p, p, p)
     assert st == -1, case
 
 

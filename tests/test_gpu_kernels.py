@@ -137,6 +137,57 @@ def test_attention(dtype, B, N, H, causal, fa, monkeypatch):
         assert rel(dqkv[:, sl], g[:, sl]) < TOL[dtype] * 2, nm
 
 
+@pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 50, 12, False), (2, 197, 12, False),
+                                           (3, 77, 8, True), (3, 150, 2, True), (2, 257, 16, False),
+                                           (3, 288, 2, False), (90, 197, 12, False), (130, 77, 8, True),
+                                           # N > 288: the exact-f32 kernels
+                                           (2, 400, 3, False)])
+def test_attention_x3(B, N, H, causal):
+    """The bf16x3 mode's attention (attention_x3.hip: every product as three bf16 MFMA products of the hi / lo
+    splits) against an fp64 reference: ~2^-16 relative per product, held to 1e-4 (O, lse) and 3e-4 (dq, dk,
+    dv) -- the bf16 kernels' bound is 3e-2."""
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 11, torch.float32)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(12)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    o = torch.empty(B * N, D, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_attention_fwd_x3", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(),
+           mask.data_ptr() if mask is not None else None, int(causal), B, H, N, D)
+    qr = qkv.double().requires_grad_(True)
+    oref, lref = attn_ref64(qr, B, N, H, mask, causal)
+    e_o, e_l = rel(o, oref), (lse.double() - lref).abs().max().item()
+    do = rnd((B * N, D), 13, torch.float32)
+    oref.backward(do.double())
+    dqkv = torch.empty_like(qkv)
+    T.call("clipmi_attention_bwd_x3", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+           dqkv.data_ptr(), mask.data_ptr() if mask is not None else None, int(causal), B, H, N, D)
+    g = qr.grad
+    e_g = [rel(dqkv[:, i * D:(i + 1) * D], g[:, i * D:(i + 1) * D]) for i in range(3)]
+    print(f"\n[x3 attention B={B} N={N} H={H} causal={causal}] O {e_o:.2e} lse {e_l:.2e} dq/dk/dv {e_g}")
+    assert e_o < 1e-4 and e_l < 1e-4, (e_o, e_l)
+    assert max(e_g) < 3e-4, e_g
+
+
+def attn_ref64(qkv, B, N, H, mask, causal):
+    D = H * 64
+    q, k, v = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / 8.0
+    blocked = torch.zeros(B, 1, N, N, dtype=torch.bool, device=qkv.device)
+    if causal:
+        blocked |= torch.triu(torch.ones(N, N, dtype=torch.bool, device=qkv.device), 1)
+    if mask is not None:
+        blocked |= (mask == 0)[:, None, None, :]
+    s = s.masked_fill(blocked, float("-inf"))
+    p = torch.softmax(s, -1)
+    o = (p @ v).transpose(1, 2).reshape(B * N, D)
+    return o, torch.logsumexp(s, -1).reshape(-1)
+
+
 @pytest.mark.parametrize("B,N,H,causal", [(2, 197, 12, False), (90, 197, 12, False), (3, 150, 2, True),
                                            (2, 224, 3, False), (2, 129, 2, False)])
 def test_attention_bwd_single_pass(B, N, H, causal, monkeypatch):
@@ -485,7 +536,10 @@ def _adapter_torch(x, sd, ln):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("R,D,A,ln", [(1024, 768, 256, True), (1000, 1024, 256, True), (77, 512, 64, False),
-                                      (1, 512, 256, True)])
+                                      (1, 512, 256, True),
+                                      # bottleneck / hidden widths that are not multiples of 8 (nn.Linear takes
+                                      # any): fp32 runs them, bf16 (16-byte MFMA rows) refuses with ValueError
+                                      (64, 768, 100, True), (33, 512, 99, True), (16, 100, 37, False)])
 def test_adapter_fused_pooled_rows_matches_torch(dtype, R, D, A, ln):
     """clipmi_adapter_fwd / clipmi_adapter_bwd at the pooled-row sizes of the bench configs (R = the
     per-GPU batch, ragged R = 1000, a single row) vs an fp32 PyTorch autograd run of the same
@@ -519,6 +573,10 @@ def test_adapter_fused_pooled_rows_matches_torch(dtype, R, D, A, ln):
         torch.cuda.synchronize()
         return y, dx, gr
 
+    if dtype == torch.bfloat16 and (D % 8 or A % 8):
+        with pytest.raises(ValueError, match="multiples of 8"):
+            run()
+        return
     y, dx, gr = run()
     y2, dx2, gr2 = run()
     assert torch.equal(y, y2) and torch.equal(dx, dx2) and all(torch.equal(gr[k], gr2[k]) for k in names)
@@ -632,3 +690,42 @@ def test_resize_u8_matches_oracle_random_sizes():
         out = T.resize_uint8(torch.from_numpy(img).cuda(), oh, ow).cpu().numpy()
         ref = np.stack([RR.resize_bicubic(im, oh, ow) for im in img])
         assert np.array_equal(out, ref), (h, w, oh, ow)
+
+
+def test_gemm_batched_beyond_grid_z_limit():
+    """clipmi_gemm_batched with nb1 * nb2 > 65535 (e.g. peclip's general head width at B = 8192 x 8 heads): the
+    wrapper splits the batch over several launches (grid z is capped at 65535); every product vs torch."""
+    nb1, nb2, M, N, K = 8500, 8, 5, 6, 7
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(nb1, nb2, M, K, generator=g).cuda()
+    B = torch.randn(nb1, nb2, N, K, generator=g).cuda()
+    C = torch.full((nb1, nb2, M, N), float("nan"), device="cuda")
+    kern.gemm_batched(M, N, K, A, K, True, B, K, True, C, N, nb1, nb2, (nb2 * M * K, M * K), (nb2 * N * K, N * K),
+                      (nb2 * M * N, M * N))
+    ref = A @ B.transpose(-1, -2)
+    assert rel(C, ref) < 2e-5
+
+
+def test_layernorm_bwd_any_width_lds_grows():
+    """ln_bwd_any_kernel's dynamic LDS (32 * D bytes with affine gradients) is opted in by the largest size asked
+    so far: a small-D call first, then D = 4000 (125 KiB), both against torch."""
+    for D in (96, 4000):
+        R = 40
+        x = rnd((R, D), D, torch.float32)
+        w = rnd((D,), D + 1, torch.float32) * 0.2 + 1
+        b = rnd((D,), D + 2, torch.float32) * 0.1
+        dy = rnd((R, D), D + 3, torch.float32)
+        y = torch.empty_like(x)
+        st = torch.empty(2, R, device="cuda")
+        s = kern.stream()
+        T.call("clipmi_layernorm_fwd", s, F32, x.data_ptr(), D, y.data_ptr(), D, w.data_ptr(), b.data_ptr(),
+               st[0].data_ptr(), st[1].data_ptr(), R, D, 1e-5, None, None, 0)
+        dx = torch.empty_like(x)
+        dw, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+        ws = T._ws(T._lib.lib().clipmi_layernorm_bwd_ws(R, D), "cuda")
+        T.call("clipmi_layernorm_bwd", s, F32, dy.data_ptr(), D, x.data_ptr(), D, st[0].data_ptr(), st[1].data_ptr(),
+               w.data_ptr(), dx.data_ptr(), D, None, 0, dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(), ws.numel(),
+               R, D)
+        xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+        F.layer_norm(xr, (D,), wr, br, 1e-5).backward(dy)
+        assert rel(dx, xr.grad) < 1e-4 and rel(dw, wr.grad) < 1e-4 and rel(db, br.grad) < 1e-4, D

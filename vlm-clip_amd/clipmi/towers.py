@@ -73,6 +73,8 @@ _lib.declare("clipmi_layernorm_fwd2", [c_vp, c_int, c_int, c_vp, c_i64, c_vp, c_
                                        c_int, c_float, c_vp, c_vp, c_int])
 _lib.declare("clipmi_layernorm_bwd2", [c_vp, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
                                        c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
+_lib.declare("clipmi_layernorm_bwd3", [c_vp, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                       c_i64, c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
 _lib.declare("clipmi_layernorm_bwd_ws", [c_int, c_int], c_i64)
 _lib.declare("clipmi_layernorm_bwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
                                       c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
@@ -136,6 +138,8 @@ _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_in
 _lib.declare("clipmi_attention_fwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_int])
+_lib.declare("clipmi_attention_fwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
+_lib.declare("clipmi_attention_bwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_fwd_mxfp8", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_l2norm_fwd", [c_vp, c_vp, c_vp, c_vp, c_int, c_int])
 _lib.declare("clipmi_l2norm_bwd", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int])
@@ -436,8 +440,11 @@ class VisionTowerFn(torch.autograd.Function):
         dh0 = torch.empty(R, D, dtype=dtype, device=dev)
         lws = _ws(_lib.lib().clipmi_layernorm_bwd_ws(R, D), dev)
         g = arena.grad
-        call("clipmi_layernorm_bwd2", s, dcode(ctx.h0.dtype), dc, P_(dx), D, P_(ctx.h0), D, P_(ctx.stats0[0]),
-             P_(ctx.stats0[1]), arena.ptr("vision_model.pre_layrnorm.weight", wbuf), P_(dh0), D, None, 0,
+        # the forward's gamma: the fp32 master with the fp32 residual stream, else the shadow
+        wdc = dcode(torch.float32) if ctx.r32 else dc
+        gamma = arena.ptr("vision_model.pre_layrnorm.weight", arena.data if ctx.r32 else wbuf)
+        call("clipmi_layernorm_bwd3", s, dcode(ctx.h0.dtype), dc, wdc, P_(dx), D, P_(ctx.h0), D, P_(ctx.stats0[0]),
+             P_(ctx.stats0[1]), gamma, P_(dh0), D, None, 0,
              arena.ptr("vision_model.pre_layrnorm.weight", g), arena.ptr("vision_model.pre_layrnorm.bias", g), 1,
              P_(lws), lws.numel(), R, D)
         Kp, Kc = ctx.X.shape[1], v.num_channels * v.patch_size ** 2

@@ -45,7 +45,10 @@ int adp_gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, b
 
 int adp_check(int dtype, int R, int D, int A, int ln) {
   CLIPMI_REQUIRE(dtype == CLIPMI_BF16 || dtype == CLIPMI_F32, "adapter: bf16 or f32");
-  CLIPMI_REQUIRE(R >= 0 && D > 0 && A > 0 && D % 8 == 0 && A % 8 == 0, "adapter: D and A multiples of 8");
+  CLIPMI_REQUIRE(R >= 0 && D > 0 && A > 0, "adapter: R >= 0, D > 0, A > 0");
+  // the bf16 MFMA GEMMs stage 16-byte rows; the fp32 GEMM (exact-f32 and bf16x3 modes) takes any width,
+  // as nn.Linear does
+  CLIPMI_REQUIRE(dtype != CLIPMI_BF16 || (D % 8 == 0 && A % 8 == 0), "adapter: bf16 needs D and A multiples of 8");
   CLIPMI_REQUIRE(!ln || D <= 4096, "adapter: with the LayerNorm D <= 4096");
   return CLIPMI_OK;
 }

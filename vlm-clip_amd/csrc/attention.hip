@@ -23,6 +23,7 @@
 // f32 path: exact-f32 SIMT kernels (4 lanes per row) for the fp32 parity mode.
 #include "common.h"
 #include "internal.h"
+#include "attn_frag.h"
 #include <algorithm>
 #include <cstdlib>
 
@@ -37,29 +38,6 @@ constexpr int ATTN_MAX_N_ANY = 4096;  // K/V-streaming kernels (bf16 flash forwa
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 constexpr float NEG_INF = -__builtin_huge_valf();
-
-__device__ __forceinline__ int img_off(int r, int c) { return r * 128 + ((c ^ (r & 6)) << 4); }
-
-__device__ __forceinline__ bf16x8 frag_row(const char* img, int r, int c) {
-  return *LDS_PTR(const bf16x8, img + img_off(r, c));
-}
-
-// transposed fragment: element j<4 from rows r0+q, j>=4 from rows r0+16+q; column d0 + lane&15
-__device__ __forceinline__ bf16x8 frag_tr(const char* img, int r0, int d0, int lane) {
-  const int q = (lane & 15) >> 2;
-  const int col = d0 + 4 * (lane & 3);
-  const int ra = r0 + 4 * (lane >> 4) + q, rb = ra + 16;
-  const int c = col >> 3, h = (col & 7) * 2;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + img_off(ra, c) + h));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + img_off(rb, c) + h));
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, w);
-}
-
-__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
-  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
-}
 
 // stage rows [0, Npad) of a [N][64] head slice (row stride ld elements) into an image
 __device__ __forceinline__ void stage_img(char* img, const bf16* src, int64_t ld, int N, int Npad, int t, int nthr) {

@@ -38,6 +38,9 @@ int clipmi_attention_fwd(void*, int, const void*, void*, float*, const int64_t*,
 int clipmi_attention_bwd(void*, int, const void*, const void*, const float*, const void*, void*, const int64_t*, int,
                          int, int, int, int);
 int clipmi_quant_mxfp8(void*, int, const void*, int64_t, int64_t, int, uint8_t*, uint8_t*);
+int clipmi_attention_fwd_x3(void*, const void*, void*, float*, const int64_t*, int, int, int, int, int);
+int clipmi_attention_bwd_x3(void*, const void*, const void*, const float*, const void*, void*, const int64_t*, int,
+                            int, int, int, int);
 }
 
 namespace {
@@ -274,7 +277,10 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
     CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.x_in, D, a.ln1, D, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps,
                                      nullptr, nullptr, 0));
     CLIPMI_TRY(gemm(s, dt, R, 3 * D, D, a.ln1, D, true, w.qkv_w, D, true, a.qkv, 3 * D, dt, CLIPMI_EPI_BIAS, w.qkv_b));
-    CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    if (t_x3)  // bf16x3: the attention products split too
+      CLIPMI_TRY(clipmi_attention_fwd_x3(s, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    else
+      CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
     CLIPMI_TRY(gemm(s, dt, R, D, D, a.o, D, true, w.out_w, D, true, a.h, D, xdt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
                     w.out_b, a.x_in, D));
     CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
@@ -370,8 +376,12 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     // attention branch: g2 is dL/dh
     CLIPMI_TRY(gemm(s, dt, R, D, D, g2, D, true, w.out_w, D, false, dln, D, dt, 0));     // d_o = dh Wo
     CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w, g.out_b));                            // gWo += dh^T o
-    CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
-                                    d->N, D));                              // d_qkv
+    if (t_x3)
+      CLIPMI_TRY(clipmi_attention_bwd_x3(s, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                         d->N, D));                         // d_qkv
+    else
+      CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                      d->N, D));                            // d_qkv
     CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w, g.qkv_b));  // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
     CLIPMI_TRY(ln_guard());

@@ -1363,9 +1363,22 @@ extern "C" int clipmi_gemm_batched(void* stream, const clipmi_gemm_desc* d, int 
   CLIPMI_REQUIRE(d->ab_dtype == CLIPMI_F32 && d->c_dtype == CLIPMI_F32, "batched GEMM: fp32 operands and output");
   CLIPMI_REQUIRE((d->flags & ~CLIPMI_EPI_BETA) == 0 && d->split_k <= 1 && !d->bias_grad,
                  "batched GEMM: no epilogue besides beta, no split-K");
-  CLIPMI_REQUIRE(nb1 >= 0 && nb2 >= 0 && (int64_t)nb1 * nb2 <= 65535, "batched GEMM: 0 <= nb1 * nb2 <= 65535");
+  CLIPMI_REQUIRE(nb1 >= 0 && nb2 >= 0 && nb2 <= 65535, "batched GEMM: nb1 >= 0, 0 <= nb2 <= 65535");
   CLIPMI_REQUIRE(d->A && d->B && d->C, "batched GEMM: operands");
   if (d->M == 0 || d->N == 0 || nb1 == 0 || nb2 == 0) return CLIPMI_OK;
+  // grid z carries (i1, i2) and is capped at 65535: larger batches (e.g. B = 8192 samples x 8 heads) run as
+  // several launches over chunks of i1, each with its operands offset to the chunk's first sample
+  const int c1 = 65535 / nb2;
+  if (nb1 > c1) {
+    for (int i0 = 0; i0 < nb1; i0 += c1) {
+      clipmi_gemm_desc e = *d;
+      e.A = (const float*)d->A + (int64_t)i0 * sa1;
+      e.B = (const float*)d->B + (int64_t)i0 * sb1;
+      e.C = (float*)d->C + (int64_t)i0 * sc1;
+      CLIPMI_TRY(clipmi_gemm_batched(stream, &e, std::min(c1, nb1 - i0), nb2, sa1, sa2, sb1, sb2, sc1, sc2));
+    }
+    return CLIPMI_OK;
+  }
   GemmP p;
   memset(&p, 0, sizeof(p));
   p.M = d->M; p.N = d->N; p.K = d->K;

@@ -2,8 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <map>
 #include <mutex>
-#include <set>
 #include <string>
 #include <utility>
 #include "../../include/clipmi.h"
@@ -14,18 +14,21 @@ void clipmi_set_error(const std::string& msg);
 
 #define CLIPMI_REQUIRE(cond, msg) do { if (!(cond)) return clipmi_invalid(std::string(__func__) + ": " + (msg)); } while (0)
 #define CLIPMI_HIP(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return clipmi_fail(e_, __FILE__, __LINE__); } while (0)
-// Dynamic-LDS opt-in (hipFuncSetAttribute MaxDynamicSharedMemorySize) once per (kernel, device),
-// thread-safe; recorded only when it succeeds.
+// Dynamic-LDS opt-in (hipFuncSetAttribute MaxDynamicSharedMemorySize) per (kernel, device), thread-safe:
+// the attribute is raised whenever a launch asks for more bytes than any earlier one did (a kernel whose
+// dynamic LDS scales with its arguments, e.g. ln_bwd_any_kernel's 32 * D bytes, may first run small);
+// the largest successfully set size is recorded.
 inline hipError_t lds_optin(const void* fn, int bytes) {
   static std::mutex mu;
-  static std::set<std::pair<const void*, int>> done;
+  static std::map<std::pair<const void*, int>, int> done;
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> g(mu);
   const auto key = std::make_pair(fn, dev);
-  if (done.count(key)) return hipSuccess;
+  const auto it = done.find(key);
+  if (it != done.end() && it->second >= bytes) return hipSuccess;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  if (e == hipSuccess) done.insert(key);
+  if (e == hipSuccess) done[key] = bytes;
   return e;
 }
 

@@ -142,9 +142,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TX* x, int64_t ldx, T* y, i
 
 // dx = [dres +] rstd * (g - mean(g) - xhat * mean(g*xhat)),  g = dy * w
 // per-block partial dgamma/dbeta -> ws[blockIdx][2][D]
-template <typename TX, typename T, int PS, int NP>
+// TW: the affine weight's dtype (default T; fp32 for the vision pre_layrnorm, whose fp32-residual forward
+// normalises with the fp32 master weights)
+template <typename TX, typename T, int PS, int NP, typename TW = T>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, const TX* x, int64_t ldx,
-                                                     const float* mean, const float* rstd, const T* w,
+                                                     const float* mean, const float* rstd, const TW* w,
                                                      T* dx, int64_t lddx, const T* dres, int64_t ldres,
                                                      float* ws, int R, int D) {
   __shared__ float red[4][2][NP * PS * 64];
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
     for (int j = 0; j < PS; ++j) { pg[k][j] = 0.f; pb[k][j] = 0.f; }
   float wv[NP][PS];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) vload<T, PS>(w + (k * 64 + lane) * PS, wv[k]);
+  for (int k = 0; k < NP; ++k) vload<TW, PS>(w + (k * 64 + lane) * PS, wv[k]);
   // rows per wave and iteration, every load of them (dres, dy, x) issued before the first
   // reduction (as ln_fwd_kernel).  Two rows for D <= 512 (text: 67 -> 65 us at R = 78,848); one for
   // wider rows, where two rows' registers (164 VGPRs at D = 768) cost a wave per SIMD and measured
@@ -273,9 +275,9 @@ __global__ __launch_bounds__(256) void ln_fwd_any_kernel(TX* x, int64_t ldx, T* 
 
 // dx = [dres +] rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partial dgamma /
 // dbeta -> ws[blockIdx][2][D] (each wave's own LDS row pair, summed in wave order: deterministic)
-template <typename TX, typename T>
+template <typename TX, typename T, typename TW = T>
 __global__ __launch_bounds__(256) void ln_bwd_any_kernel(const T* dy, int64_t lddy, const TX* x, int64_t ldx,
-                                                         const float* mean, const float* rstd, const T* w, T* dx,
+                                                         const float* mean, const float* rstd, const TW* w, T* dx,
                                                          int64_t lddx, const T* dres, int64_t ldres, float* ws, int R,
                                                          int D) {
   extern __shared__ float red_any[];  // [4 waves][2][D] when ws
@@ -422,6 +424,17 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* x, int64_t
     for (int j = 0; j < 4; ++j) s[j] += v[j];
   }
   store4(ws + (int64_t)blockIdx.y * N + c, s);
+}
+// the same, one column per thread: any N, ldx and alignment (fp32 adapters of any bottleneck width)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial1_kernel(const T* x, int64_t ldx, int R, int N, int rows_per,
+                                                              float* ws) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += (float)x[(int64_t)r * ldx + c];
+  ws[(int64_t)blockIdx.y * N + c] = s;
 }
 
 // periodic row sums: out[t][c] (+)= sum_b x[(b*period + t)*ldx + c]   (position-embedding grads)
@@ -605,22 +618,29 @@ void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t*
 // grid (in: the partial-sum rows the workspace holds; out: the blocks launched = partial rows
 // written): at most the blocks the CUs hold at once, so no block starts a second round late
 // (the D = 768 form keeps two rows' loads in registers: 164 VGPRs, 3 waves per SIMD)
-template <typename TX, typename T, int PS, int NP>
+template <typename TX, typename T, int PS, int NP, typename TW = T>
 void ln_bwd_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
                    int64_t ldres, float* ws, int R, int D) {
   static int resident = [] {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<TX, T, PS, NP>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<TX, T, PS, NP, TW>, 256, 0) !=
             hipSuccess || per_cu < 1)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     return per_cu * cus;
   }();
   if (grid > resident) grid = resident;
-  hipLaunchKernelGGL((ln_bwd_kernel<TX, T, PS, NP>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const TX*)x, ldx,
-                     mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
+  hipLaunchKernelGGL((ln_bwd_kernel<TX, T, PS, NP, TW>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const TX*)x,
+                     ldx, mean, rstd, (const TW*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
+}
+
+template <typename TX, typename T, int PS, int NP>
+void ln_bwd_launch_w32(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                       const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
+                       int64_t ldres, float* ws, int R, int D) {
+  ln_bwd_launch<TX, T, PS, NP, float>(s, grid, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, ws, R, D);
 }
 
 // the widths the register-resident kernels take
@@ -710,18 +730,21 @@ extern "C" int64_t clipmi_layernorm_bwd_ws(int R, int D) {
   return (int64_t)nb * 2 * D * 4;
 }
 
-template <typename TX, typename T>
+template <typename TX, typename T, typename TW = T>
 static int ln_bwd_t(hipStream_t s, int& nb, const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* mean,
                     const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres, int64_t ldres, float* wsf,
                     int R, int D) {
   if (!ln_fast_width(D)) {
     const size_t lds = wsf ? (size_t)4 * 2 * D * 4 : 0;
-    (void)lds_optin((const void*)ln_bwd_any_kernel<TX, T>, (int)lds);
-    hipLaunchKernelGGL((ln_bwd_any_kernel<TX, T>), dim3(nb), dim3(256), lds, s, (const T*)dy, lddy, (const TX*)x, ldx,
-                       mean, rstd, (const T*)w, (T*)dx, lddx, (const T*)dres, ldres, wsf, R, D);
+    (void)lds_optin((const void*)ln_bwd_any_kernel<TX, T, TW>, (int)lds);
+    hipLaunchKernelGGL((ln_bwd_any_kernel<TX, T, TW>), dim3(nb), dim3(256), lds, s, (const T*)dy, lddy, (const TX*)x, ldx,
+                       mean, rstd, (const TW*)w, (T*)dx, lddx, (const T*)dres, ldres, wsf, R, D);
     return CLIPMI_OK;
   }
-  LN_DISPATCH(D, ln_bwd_launch, TX, T, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  if constexpr (std::is_same<TW, T>::value)
+    LN_DISPATCH(D, ln_bwd_launch, TX, T, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
+  else
+    LN_DISPATCH(D, ln_bwd_launch_w32, TX, T, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D);
   return CLIPMI_OK;
 }
 
@@ -737,8 +760,20 @@ extern "C" int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const
                                      int64_t ldx, const float* mean, const float* rstd, const void* w, void* dx,
                                      int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db, int beta_wb,
                                      void* ws, int64_t ws_bytes, int R, int D) {
+  return clipmi_layernorm_bwd3(stream, x_dtype, dtype, dtype, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, dw,
+                               db, beta_wb, ws, ws_bytes, R, D);
+}
+
+// w_dtype: the affine weight's dtype -- dtype, or fp32 with fp32 x and bf16 gradients (a LayerNorm whose forward
+// normalised with fp32 master weights, e.g. the vision pre_layrnorm on the fp32 residual stream)
+extern "C" int clipmi_layernorm_bwd3(void* stream, int x_dtype, int dtype, int w_dtype, const void* dy, int64_t lddy,
+                                     const void* x, int64_t ldx, const float* mean, const float* rstd, const void* w,
+                                     void* dx, int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db,
+                                     int beta_wb, void* ws, int64_t ws_bytes, int R, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(ln_types_ok(x_dtype, dtype), "layernorm: dtypes (equal, or fp32 x with bf16 gradients)");
+  CLIPMI_REQUIRE(w_dtype == dtype || (w_dtype == CLIPMI_F32 && x_dtype == CLIPMI_F32),
+                 "layernorm: weight dtype (the gradients', or fp32 with fp32 x)");
   CLIPMI_REQUIRE(D >= 1 && D <= LN_ANY_MAX_D, "D must be in [1, 4096]");
   if (R == 0) return CLIPMI_OK;
   int nb = (R + 3) / 4;
@@ -747,6 +782,8 @@ extern "C" int clipmi_layernorm_bwd2(void* stream, int x_dtype, int dtype, const
   if (wsf) CLIPMI_REQUIRE(ws_bytes >= (int64_t)nb * 2 * D * 4, "layernorm_bwd workspace too small");
   // the fast kernels shrink nb to the resident block count (the partial rows they write)
   if (dtype == CLIPMI_F32) CLIPMI_TRY((ln_bwd_t<float, float>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
+  else if (x_dtype == CLIPMI_F32 && w_dtype == CLIPMI_F32)
+    CLIPMI_TRY((ln_bwd_t<float, bf16, float>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
   else if (x_dtype == CLIPMI_F32) CLIPMI_TRY((ln_bwd_t<float, bf16>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
   else CLIPMI_TRY((ln_bwd_t<bf16, bf16>(s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R, D)));
   CLIPMI_CHECK_LAUNCH();
@@ -788,16 +825,26 @@ extern "C" int64_t clipmi_colsum_ws(int R, int N) {
 extern "C" int clipmi_colsum(void* stream, int dtype, const void* x, int64_t ldx, int R, int N, float* out, int beta,
                              void* ws, int64_t ws_bytes) {
   hipStream_t s = (hipStream_t)stream;
-  CLIPMI_REQUIRE(N % 4 == 0 && ldx % 4 == 0, "N, ldx must be multiples of 4");
+  CLIPMI_REQUIRE(N >= 0 && ldx >= N, "colsum: N >= 0, ldx >= N");
   int chunks = (R + 255) / 256;
   if (chunks > 512) chunks = 512;
   if (chunks < 1) chunks = 1;
   CLIPMI_REQUIRE(ws_bytes >= (int64_t)chunks * N * 4, "colsum workspace too small");
+  if (N == 0) return CLIPMI_OK;
   int rows_per = (R + chunks - 1) / chunks;
+  const size_t al = dtype == CLIPMI_BF16 ? 8 : 16;  // load4's vector width
+  if (N % 4 || ldx % 4 || ((uintptr_t)x & (al - 1))) {
+    dim3 g1((N + 255) / 256, chunks);
+    if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(colsum_partial1_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)x, ldx, R, N, rows_per, (float*)ws);
+    else hipLaunchKernelGGL(colsum_partial1_kernel<float>, g1, dim3(256), 0, s, (const float*)x, ldx, R, N, rows_per, (float*)ws);
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
+    CLIPMI_CHECK_LAUNCH();
+    return CLIPMI_OK;
+  }
   dim3 g((N / 4 + 255) / 256, chunks);
   if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)x, ldx, R, N, rows_per, (float*)ws);
   else hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, s, (const float*)x, ldx, R, N, rows_per, (float*)ws);
-  if (((uintptr_t)ws & 15) == 0)
+  if (((uintptr_t)ws & 15) == 0 && N % 4 == 0)
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, (float*)nullptr, beta);
   else
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N, chunks, N, out, beta);
