@@ -10,7 +10,7 @@ checkpoint format and error types as the reference; the compute runs on libclipm
                kernels: north_star's 1e-3 logits at several times the fp32 mode's speed) or "fp8" (frozen
                towers with MXFP8 GEMMs, BASELINE config 5; adapters and the loss stay bf16 / fp32)
   residual_fp32  bf16 mode: keep the towers' residual stream (each layer's input, the attention-branch sum)
-               in fp32 -- default when the towers are trained (freeze_clip=False), bf16 when they are frozen
+               in fp32 (default; False keeps it in bf16, ~7 % faster on the frozen-tower adapter configs)
   pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
                (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
   init_seed    seed of the deterministic random init used when no weights file exists
@@ -129,11 +129,12 @@ class CLIPWithAdapters(nn.Module):
                                                   for i in range(shared_adapter_layers)])
         self._rt = _Runtime(self.clip, dtype)
         self._rt.fp8 = precision == "fp8"
-        # bf16 mode: the towers' residual stream in fp32 (engine resid_f32; profiles/r05_bf16_error_sources.log)
-        # when the towers are trained (full fine-tune, BASELINE config 3); frozen towers (the adapter configs)
-        # keep it in bf16, where the fp32 stream's 12 extra bytes per element and layer cost 7 % of the step
+        # bf16 mode: the towers' residual stream in fp32 (engine resid_f32; profiles/r05_bf16_error_sources.log),
+        # trained or frozen: at config 4's model and batch (L/14, B = 1024) the bf16 stream measured max |dlogit|
+        # 0.236 against PyTorch autocast's 0.066 (profiles/r06_config4_frozen_vs_amp.log); its 12 extra bytes per
+        # element and layer cost ~7 % of the frozen-tower step
         if residual_fp32 is None:
-            residual_fp32 = not freeze_clip
+            residual_fp32 = True
         self._rt.resid32 = precision == "bf16" and bool(residual_fp32)
         # bf16x3: the towers' GEMMs (patch embedding, every encoder GEMM) as split-operand bf16 products
         self._rt.x3 = precision == "bf16x3"
