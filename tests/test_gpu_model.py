@@ -290,8 +290,8 @@ def test_b16_full_finetune_gradients_fp32(golden):
     bound = 2 * (2e-4 + eps_c)
     print(f"\n[b16 full fp32] vs the reference's fp32 run: largest grad errs {[(round(e, 6), n) for e, n in errs[:4]]}\n"
           f"  vs the fp64 oracle: this run {e_gpu}, the reference's fp32 run {e_ref}; loss-gradient conditioning "
-          f"eps_c {eps_c}; bound {bound:.3e} (headroom {bound / e_gpu[0]:.2f}x)")
-    assert e_gpu[0] < bound, (e_gpu, eps_c)
+          f"eps_c {eps_c}; bound {bound:.3e} (headroom {bound / e_gpu[0][0]:.2f}x)")
+    assert e_gpu[0][0] < bound, (e_gpu, eps_c)
 
 
 def _fp64_oracle_errors(m, g, s, gmax, out):
@@ -308,13 +308,14 @@ def _fp64_oracle_errors(m, g, s, gmax, out):
         loss = R.contrastive(tf, imf, p["logit_scale"])["loss"]
     loss.backward()
     params = dict(m.named_parameters())
-    e_gpu, e_ref = (0.0, ""), (0.0, "")
+    e_gpu, e_ref = [], []
     for n, (kind, ref, idx) in s.items():
         exact = _take(kind, p[n].grad, idx).astype(np.float64)
         got = _take(kind, params["clip." + n].grad, idx)
         scale = max(float(np.abs(exact).max()), 0.05 * gmax, 1e-8)
-        e_gpu = max(e_gpu, (float(np.abs(got - exact).max()) / scale, n))
-        e_ref = max(e_ref, (float(np.abs(ref - exact).max()) / scale, n))
+        e_gpu.append((float(np.abs(got - exact).max()) / scale, n))
+        e_ref.append((float(np.abs(ref - exact).max()) / scale, n))
+    e_gpu, e_ref = sorted(e_gpu, reverse=True)[:3], sorted(e_ref, reverse=True)[:3]
 
     def loss_grads(t, i):
         t, i = t.detach().clone().requires_grad_(True), i.detach().clone().requires_grad_(True)

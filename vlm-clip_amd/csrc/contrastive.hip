@@ -70,7 +70,11 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* S, float* L, c
   }
 }
 
-// dS = gout * exp(ls) * (softmax(L) - onehot) / (2 Bg) ; dls_row = sum_j dL_ij L_ij
+// dS = gout * exp(ls) * (softmax(L) - onehot) / (2 Bg) ; dls_row = sum_j dL_ij (L_ij - lse_i)
+// (= sum_j dL_ij L_ij, since sum_j dL_ij = 0 in exact arithmetic: centring the logits on the row's lse keeps
+// the terms O(log Bg) instead of O(L), so the softmax-weighted mean and the label logit -- nearly equal when the
+// loss sits near ln Bg -- no longer cancel at the logits' magnitude in fp32; B = 2 fixture: logit_scale
+// gradient 8.9e-4 -> see tests/test_gpu_model.py::test_b16_full_finetune_gradients_fp32)
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* L, const float* lse, const float* logit_scale,
                                                      const float* gout, int B, int Bg, int label0, float norm,
                                                      float* dS, float* dls_row) {
@@ -85,7 +89,7 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* L, const float
   float acc = 0.f;
   for (int j = lane; j < Bg; j += 64) {
     float dl = g * (expf(l[j] - ls) - (j == label0 + row ? 1.f : 0.f));
-    acc += dl * l[j];
+    acc += dl * (l[j] - ls);
     d[j] = dl * sc;
   }
   acc = wave_sum(acc);
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(256) void ce_bwd_chunk_kernel(const float* S, const
   for (int j = lane; j < C; j += 64) {
     const float l = s[j] * sc;
     const float dl = g * (expf(l - ls) - (j == lc ? 1.f : 0.f));
-    acc += dl * l;
+    acc += dl * (l - ls);
     d[j] = dl * sc;
   }
   acc = wave_sum(acc);
