@@ -279,34 +279,38 @@ def test_b16_full_finetune_gradients_fp32(golden):
         errs.append((float(np.abs(got - ref).max()) / scale, n))
     errs.sort(reverse=True)
     worst = errs[0]
-    # The bound is derived from this fixture's conditioning, measured on this run against exact arithmetic: the
-    # oracle (oracle/clip_ref.py, pinned to the reference) run in fp64 on the same weights and batch.  The tower
-    # backward maps the contrastive loss's feature gradient to every parameter gradient and is pinned at 2e-4 on
-    # the well-conditioned fixture (test_b16_feature_gradients_fp32); what this fixture adds is the loss's
-    # sensitivity to the features: eps_c = the change of the fp64 loss gradients (w.r.t. the normalised features
-    # and logit_scale, model_m.py:146-163) between this run's fp32 features and the exact ones.  Bound: twice
-    # the error model, 2 * (2e-4 + eps_c).  The reference's own fp32 run (the golden) is measured the same way.
-    e_gpu, e_ref, eps_c = _fp64_oracle_errors(m, g, s, gmax, out)
-    bound = 2 * (2e-4 + eps_c)
+    # The bound is derived from this fixture's conditioning, measured on this run against exact arithmetic (the
+    # oracle, oracle/clip_ref.py, pinned to the reference, run in fp64 on the same weights and batch).  Under
+    # quirk Q1 the two captions are identical and the loss sits at ln 2, so the two samples' loss gradients
+    # (w.r.t. each caption's and each image's features, model_m.py:146-163) are nearly opposite, and every
+    # parameter gradient is the small sum of two large per-sample contributions: per-sample errors are amplified
+    # by kappa = max_b |g_b| / |sum_b g_b| (fp64, max over both modalities).  The fp32 backward's per-sample error is
+    # pinned by the well-conditioned fixture (test_b16_feature_gradients_fp32: 1.8e-5, rounded up to 2e-5), so the
+    # bound is twice the error model: 2 * kappa * 2e-5.  The reference's own fp32 run (the golden) is measured the
+    # same way, beside this run.
+    e_gpu, e_ref, kappa = _fp64_oracle_errors(m, g, s, gmax)
+    bound = 2 * kappa * 2e-5
     print(f"\n[b16 full fp32] vs the reference's fp32 run: largest grad errs {[(round(e, 6), n) for e, n in errs[:4]]}\n"
-          f"  vs the fp64 oracle: this run {e_gpu}, the reference's fp32 run {e_ref}; loss-gradient conditioning "
-          f"eps_c {eps_c}; bound {bound:.3e} (headroom {bound / e_gpu[0][0]:.2f}x)")
-    assert e_gpu[0][0] < bound, (e_gpu, eps_c)
+          f"  vs the fp64 oracle: this run {e_gpu}, the reference's fp32 run {e_ref}; per-sample cancellation "
+          f"kappa {kappa:.1f}; bound {bound:.3e} (headroom {bound / e_gpu[0][0]:.2f}x)")
+    assert e_gpu[0][0] < bound, (e_gpu, kappa)
 
 
-def _fp64_oracle_errors(m, g, s, gmax, out):
-    """Against the oracle in fp64 on the GPU: (worst error of this run's sampled gradients, worst error of the
-    golden's, eps_c) with the test's scale convention; eps_c = max relative change of the fp64 contrastive
-    gradients (normalised features: max-abs relative; logit_scale: relative to the test's scale floor) between
-    this run's features and the exact ones."""
+def _fp64_oracle_errors(m, g, s, gmax):
+    """Against the oracle in fp64 on the GPU: (3 worst errors of this run's sampled gradients, 3 worst of the
+    golden's) with the test's scale convention, and kappa = the per-sample cancellation of the contrastive loss's
+    feature gradients, max over modalities of max_b |g_b| / |sum_b g_b| (max-abs norms)."""
     from oracle import clip_ref as R
     p = {n[5:]: t.detach().double().clone().requires_grad_(True) for n, t in m.named_parameters()}
     b = {k: v.to(torch.float64) if v.is_floating_point() else v for k, v in batch(m.config, 2, g).items()}
     with torch.device("cuda"):
         tf = R.text_features(b["input_ids"], b["attention_mask"], p, m.config)
         imf = R.image_features(b["pixel_values"], p, m.config)
+        tf.retain_grad()
+        imf.retain_grad()
         loss = R.contrastive(tf, imf, p["logit_scale"])["loss"]
     loss.backward()
+    kappa = max(float(f.grad.abs().max() / f.grad.sum(0).abs().max()) for f in (tf, imf))
     params = dict(m.named_parameters())
     e_gpu, e_ref = [], []
     for n, (kind, ref, idx) in s.items():
@@ -315,22 +319,7 @@ def _fp64_oracle_errors(m, g, s, gmax, out):
         scale = max(float(np.abs(exact).max()), 0.05 * gmax, 1e-8)
         e_gpu.append((float(np.abs(got - exact).max()) / scale, n))
         e_ref.append((float(np.abs(ref - exact).max()) / scale, n))
-    e_gpu, e_ref = sorted(e_gpu, reverse=True)[:3], sorted(e_ref, reverse=True)[:3]
-
-    def loss_grads(t, i):
-        t, i = t.detach().clone().requires_grad_(True), i.detach().clone().requires_grad_(True)
-        ls = p["logit_scale"].detach().clone().requires_grad_(True)
-        with torch.device("cuda"):
-            L = R.contrastive(t, i, ls)["loss"]
-        L.backward()
-        return t.grad, i.grad, ls.grad
-
-    nt = lambda x: x / x.norm(dim=-1, keepdim=True)
-    ex = loss_grads(nt(tf), nt(imf))
-    run = loss_grads(out["text_features"].detach().double(), out["image_features"].detach().double())
-    eps = [float((run[k] - ex[k]).abs().max() / ex[k].abs().max()) for k in range(2)]
-    eps.append(float((run[2] - ex[2]).abs()) / max(float(ex[2].abs()), 0.05 * gmax))
-    return e_gpu, e_ref, max(eps)
+    return sorted(e_gpu, reverse=True)[:3], sorted(e_ref, reverse=True)[:3], kappa
 
 
 def test_b16_feature_gradients_fp32(golden):
