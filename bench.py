@@ -64,6 +64,11 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=32,
                     help="pairs per CPU-baseline step (SURVEY 8d: B = 32; 0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--comm", default="torch", choices=["torch", "clipmi"],
+                    help="N > 1: the data-parallel exchanges through torch.distributed's RCCL (default) or RCCL issued "
+                         "by libclipmi (clipmi.comm.Communicator bootstrapped over the same store)")
+    ap.add_argument("--grad-bucket-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="N > 1: dtype the gradient buckets are all-reduced in (bf16: half the bytes per ring)")
     ap.add_argument("--parity-steps", type=int, default=5,
                     help="N=1, bf16 full fine-tune: also time this many steps of the bf16x3 mode (the mode that meets "
                          "north_star's 1e-3 logits) in the same run, reported under `parity_mode` (0 = skip)")
@@ -361,6 +366,9 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
+        if args.comm == "clipmi":
+            from clipmi.comm import Communicator
+            group = Communicator.from_process_group(dist.group.WORLD)
 
     from clipmi import CLIPWithAdapters
     from clipmi import _lib
@@ -374,7 +382,8 @@ def main():
                              use_shared_adapters=False, freeze_clip=adapters, device=dev, precision=args.precision,
                              fast_init=True, process_group=group)
     params = [p for n, p in model.named_parameters() if p.requires_grad]
-    opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas(), process_group=group)
+    opt = FusedAdamW(params, lr=5e-5, weight_decay=0.01, arenas=model.arenas(), process_group=group,
+                     grad_bucket_dtype=torch.bfloat16 if args.grad_bucket_dtype == "bf16" else torch.float32)
     opt.overlap_with(model)  # world > 1: gradient buckets all-reduced under the backward (armed_backward)
     batch = synthetic_batch(cfg, args.batch, rank, dev)
     total = args.warmup + args.steps
@@ -475,7 +484,9 @@ def main():
                                f" contrastive step: fwd+bwd+all-reduce+clip+AdamW",
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": cfg.vision_config.image_size,
-                   "text_len": 77, "parallelism": f"dp{world}"},
+                   "text_len": 77, "parallelism": f"dp{world}",
+                   "comm": f"{'libclipmi' if args.comm == 'clipmi' else 'torch.distributed'} RCCL, "
+                           f"{args.grad_bucket_dtype} gradient buckets" if world > 1 else None},
         # bf16x3: the model's flops against a third of the bf16 peak (three bf16 products per fp32 one)
         "mfma_frac_step": round(value * step_flops_pair / (world * {"fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_FP32_TFLOPS,
                                                                     "bf16x3": PEAK_BF16_TFLOPS / 3}

@@ -407,6 +407,9 @@ int clipmi_comm_destroy(void* comm);
 int clipmi_allgather_embed(void* stream, void* comm, int dtype, const void* local, void* global, int64_t count);
 int clipmi_reducescatter_grad(void* stream, void* comm, int dtype, const void* global, void* local, int64_t count);
 int clipmi_allreduce_grads(void* stream, void* comm, float* grads, int64_t count);
+/* in-place sum over the ranks, fp32 or bf16 (the product path's optional bf16 gradient buckets: half the
+   bytes per ring, ~2^-9 relative rounding of each rank's contribution) */
+int clipmi_allreduce(void* stream, void* comm, int dtype, void* buf, int64_t count);
 
 #ifdef __cplusplus
 }

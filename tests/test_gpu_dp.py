@@ -13,16 +13,16 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False, backend="gloo"):
+def _worker(rank, world, port, q, overlap=False, chunk=None, shared=False, backend="gloo", bucket=None):
     try:
-        _worker_body(rank, world, port, q, overlap, chunk, shared, backend)
+        _worker_body(rank, world, port, q, overlap, chunk, shared, backend, bucket)
     except BaseException:  # report instead of leaving the parent waiting on the queue
         import traceback
         q.put((rank, None, traceback.format_exc()))
         raise
 
 
-def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo"):
+def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo", bucket=None):
     import sys
     if chunk is not None:  # column-streamed contrastive: Bg = 8 in chunks of 3, 3, 2
         os.environ["CLIPMI_CE_CHUNK"] = str(chunk)
@@ -34,28 +34,34 @@ def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo"):
     from clipmi.trainer import FusedAdamW
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    # gloo: both ranks on cuda:0; nccl (= RCCL): one GPU per rank, the backend production uses
-    dev = f"cuda:{rank}" if backend == "nccl" else "cuda:0"
+    # gloo: both ranks on cuda:0; nccl (= RCCL through torch) and clipmi (RCCL issued by libclipmi, a
+    # clipmi.comm.Communicator bootstrapped over a gloo group's store): one GPU per rank
+    dev = f"cuda:{rank}" if backend in ("nccl", "clipmi") else "cuda:0"
     torch.cuda.set_device(dev)
-    dist.init_process_group(backend, rank=rank, world_size=world)
+    dist.init_process_group("gloo" if backend == "clipmi" else backend, rank=rank, world_size=world)
+    group = dist.group.WORLD
+    if backend == "clipmi":
+        from clipmi.comm import Communicator
+        group = Communicator.from_process_group(dist.group.WORLD)
     # shared adapters need text hidden 512 (their text_projection, model_m.py:54-61): B/32
     m = CLIPWithAdapters("B/32" if shared else "tiny", use_text_adapter=True, use_vision_adapter=True,
                          use_shared_adapters=shared,
                          freeze_clip=False, device=dev, precision="fp32", pooling="eos",
-                         process_group=dist.group.WORLD)
+                         process_group=group)
     if shared:
         m.eval()  # shared-adapter dropout off: the ranks must reproduce the single-device gradients
     B = 4
     b = {k: torch.from_numpy(v).to(dev) for k, v in synth.synthetic_batch(m.config, B, seed=5, start=rank * B).items()}
     if overlap:  # gradient buckets all-reduced from the towers' chunked backward (GradBucketReducer)
         opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas(),
-                         process_group=dist.group.WORLD).overlap_with(m)
+                         process_group=group,
+                         grad_bucket_dtype=torch.bfloat16 if bucket == "bf16" else torch.float32).overlap_with(m)
     else:
         opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, arenas=m.arenas())
     opt.zero_grad()
     out = m(**b)
     opt.armed_backward(out["loss"])
-    opt.grads_all_reduce(dist.group.WORLD)
+    opt.grads_all_reduce(group)
     torch.cuda.synchronize()
     g = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters() if p.grad is not None}
     q.put((rank, out["loss"].item(), g))
@@ -67,12 +73,14 @@ def _worker_body(rank, world, port, q, overlap, chunk, shared, backend="gloo"):
                                                           (False, 3, False, "gloo"), (True, None, True, "gloo"),
                                                           # RCCL, one GPU per rank: the comm-stream ordering the
                                                           # overlapped reducer relies on
-                                                          (True, None, False, "nccl"), (False, 3, False, "nccl")])
+                                                          (True, None, False, "nccl"), (False, 3, False, "nccl"),
+                                                          # RCCL issued by libclipmi (clipmi.comm.Communicator)
+                                                          (True, None, False, "clipmi"), (False, 3, False, "clipmi")])
 def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared, backend):
     """shared=True: shared adapters on an unfrozen CLIP add a position-embedding gradient after the
     vision tower's backward, so the overlapped reducer must leave that block to finish().
     backend nccl needs two visible GPUs (skipped on a one-GPU box)."""
-    if backend == "nccl" and torch.cuda.device_count() < 2:
+    if backend in ("nccl", "clipmi") and torch.cuda.device_count() < 2:
         pytest.skip("RCCL ranks need one GPU each")
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
@@ -80,6 +88,7 @@ def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared, ba
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500
     port += 37 * int(overlap) + 71 * int(chunk is not None) + 113 * int(shared) + 157 * int(backend == "nccl")
+    port += 211 * int(backend == "clipmi")
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, chunk, shared, backend)) for r in range(2)]
     for p in procs:
         p.start()
@@ -114,19 +123,23 @@ def test_two_rank_data_parallel_matches_single_device(overlap, chunk, shared, ba
         assert worst[0] < 1e-4, worst
 
 
-@pytest.mark.parametrize("overlap,chunk", [(True, None), (False, 3)])
-def test_one_rank_rccl_group_matches_single_device(overlap, chunk):
-    """The RCCL (backend nccl) branches of the data-parallel path -- the embedding all-gather and
-    gradient reduce-scatter around the contrastive loss, the bucketed all-reduce from the comm stream
-    (overlap) or after the backward -- executed where only one GPU is visible: a one-rank group with
-    CLIPMI_DP_FORCE_COLLECTIVES=1 takes every collective branch, each then the identity, so the result
-    must equal the group-free run on the same 4 samples."""
+@pytest.mark.parametrize("overlap,chunk,backend,bucket", [(True, None, "nccl", None), (False, 3, "nccl", None),
+                                                          (True, None, "clipmi", None), (False, 3, "clipmi", None),
+                                                          (True, None, "clipmi", "bf16")])
+def test_one_rank_rccl_group_matches_single_device(overlap, chunk, backend, bucket):
+    """The RCCL branches of the data-parallel path -- the embedding all-gather and gradient reduce-scatter
+    around the contrastive loss, the bucketed all-reduce from the comm stream (overlap) or after the backward
+    -- executed where only one GPU is visible: a one-rank group with CLIPMI_DP_FORCE_COLLECTIVES=1 takes every
+    collective branch, each then the identity, so the result must equal the group-free run on the same 4
+    samples.  backend nccl: torch.distributed's RCCL; clipmi: a clipmi.comm.Communicator, so the exchanges run
+    as clipmi_allgather_embed / clipmi_reducescatter_grad / clipmi_allreduce.  bucket bf16: the gradient buckets
+    reduced in bf16 -- at one rank each gradient comes back rounded to bf16, within 2^-8 of its scale."""
     import torch.multiprocessing as mp
     from clipmi import CLIPWithAdapters, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 30300 + os.getpid() % 500 + 37 * int(overlap)
-    p = ctx.Process(target=_worker, args=(0, 1, port, q, overlap, chunk, False, "nccl"))
+    port = 30300 + os.getpid() % 500 + 37 * int(overlap) + 71 * int(backend == "clipmi") + 113 * int(bucket is not None)
+    p = ctx.Process(target=_worker, args=(0, 1, port, q, overlap, chunk, False, backend, bucket))
     p.start()
     r = q.get(timeout=200)
     if r[1] is None:
@@ -147,4 +160,4 @@ def test_one_rank_rccl_group_matches_single_device(overlap, chunk):
     for n, v in ref.items():
         scale = max(float(np.abs(v).max()), 1e-2 * gmax)
         worst = max(worst, (float(np.abs(g[n] - v).max()) / scale, n))
-    assert worst[0] < 1e-4, worst
+    assert worst[0] < (2 ** -8 if bucket == "bf16" else 1e-4), worst

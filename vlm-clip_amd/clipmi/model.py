@@ -14,7 +14,8 @@ checkpoint format and error types as the reference; the compute runs on libclipm
   pooling      "first" (model_m.py:102 — quirk Q1, the reference behaviour) or "eos"
                (HF CLIPTextModel pooler, [HF] modeling_clip.py:561-581)
   init_seed    seed of the deterministic random init used when no weights file exists
-  process_group torch.distributed group for the data-parallel contrastive loss
+  process_group data-parallel group of the contrastive loss: a torch.distributed group (RCCL
+               through torch, or gloo) or a clipmi.comm.Communicator (RCCL issued by libclipmi)
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ import warnings
 import torch
 import torch.nn as nn
 
+from . import comm as CM
 from . import config as C
 from . import synth
 from . import towers as T
@@ -315,7 +317,7 @@ class CLIPWithAdapters(nn.Module):
             group = self.process_group
             loss, t, i, lpt, lpi = T.ContrastiveFn.apply(text_features, image_features, self.clip.logit_scale,
                                                          group, True, self.clip.arena)
-            world = torch.distributed.get_world_size(group) if group is not None else 1
+            world = CM.world_rank(group)[0]
             return {"loss": loss, "text_features": t, "image_features": i, "logits_per_text": lpt,
                     "logits_per_image": lpt.t() if world == 1 and lpt is not None else lpi}
         return {"text_features": text_features, "image_features": image_features}

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from . import comm as CM
 from . import kernels as K
 from ._lib import BF16, F32
 
@@ -720,6 +721,11 @@ def _rccl(group):
     return dist.get_backend(group) == "nccl"
 
 
+# The data-parallel group is a torch.distributed group (RCCL through torch, or gloo) or a clipmi.comm.Communicator
+# (RCCL issued by libclipmi: clipmi_allgather_embed / clipmi_reducescatter_grad / clipmi_allreduce on the caller's
+# stream).
+
+
 def force_collectives():
     """CLIPMI_DP_FORCE_COLLECTIVES=1 (tests only): a one-rank group still takes the collective branches
     (all-gather, reduce-scatter, bucketed all-reduce), each then the identity, so a one-GPU box runs
@@ -732,6 +738,8 @@ def _gather(x, group, world):
     if world == 1 and not (group is not None and force_collectives()):
         return x
     x = x.contiguous()
+    if CM.is_lib(group):
+        return group.all_gather(x)
     if _rccl(group):
         out = torch.empty(world * x.shape[0], *x.shape[1:], dtype=x.dtype, device=x.device)
         dist.all_gather_into_tensor(out, x, group=group)
@@ -748,6 +756,8 @@ def _reduce_scatter(x, group, world):
         return x
     x = x.contiguous()
     n = x.shape[0] // world
+    if CM.is_lib(group):
+        return group.reduce_scatter(x)
     if _rccl(group):
         out = torch.empty(n, *x.shape[1:], dtype=x.dtype, device=x.device)
         dist.reduce_scatter_tensor(out, x, group=group)
@@ -814,8 +824,7 @@ class ContrastiveFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, tf, imf, logit_scale, group, global_loss, arena):
-        world = dist.get_world_size(group) if group is not None else 1
-        rank = dist.get_rank(group) if group is not None else 0
+        world, rank = CM.world_rank(group)
         B, E = tf.shape
         dev = tf.device
         s = K.stream()
@@ -840,8 +849,7 @@ class ContrastiveFn(torch.autograd.Function):
             call("clipmi_sum2", s, P_(ce[0]), P_(ce[1]), B, 1.0 / (2 * Bg), P_(loss), 0)
             loss_out = loss
             if world > 1 and global_loss:
-                loss_out = loss.clone()
-                dist.all_reduce(loss_out, group=group)
+                loss_out = CM.all_reduce_(loss.clone(), group)
             ctx.save_for_backward(th, ih, tn, inn, tg, ig, lse, ls)
             ctx.group, ctx.world, ctx.B, ctx.Bg, ctx.lab0, ctx.chunk = group, world, B, Bg, lab0, C
             ctx.ls_param, ctx.arena = logit_scale, arena
@@ -858,8 +866,7 @@ class ContrastiveFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=dev)
         call("clipmi_sum2", s, P_(ce[0]), P_(ce[1]), B, 1.0 / (2 * Bg), P_(loss), 0)
         if world > 1 and global_loss:
-            loss_out = loss.clone()
-            dist.all_reduce(loss_out, group=group)
+            loss_out = CM.all_reduce_(loss.clone(), group)
         else:
             loss_out = loss
         # outputs (th, ih, lt, li) must go through save_for_backward: keeping them as plain ctx

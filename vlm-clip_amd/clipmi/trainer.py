@@ -15,6 +15,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from . import comm as CM
 from . import kernels as K
 from . import towers as T
 
@@ -35,11 +36,20 @@ class GradBucketReducer:
     backward.  ``finish`` all-reduces whatever was not reported (projections, logit_scale,
     final LNs, adapters) and makes the caller's stream wait for every bucket.  Each element is
     reduced exactly once per step.  Collectives are issued from the autograd thread in node
-    order, which is the same on every rank."""
+    order, which is the same on every rank.
 
-    def __init__(self, arenas, group=None):
+    ``group``: a torch.distributed group or a clipmi.comm.Communicator (the all-reduce then runs as
+    clipmi_allreduce on the communication stream).  ``bucket_dtype=torch.bfloat16``: each bucket is
+    reduced as bf16 (cast on the communication stream, summed, cast back into the fp32 arena): half the
+    bytes per ring (ViT-B/16 full fine-tune: 299 MB instead of 598 MB per step) at ~2^-9 relative rounding
+    of every rank's contribution."""
+
+    def __init__(self, arenas, group=None, bucket_dtype=torch.float32):
+        if bucket_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("bucket_dtype: torch.float32 or torch.bfloat16")
         self.arenas = list(arenas)
         self.group = group
+        self.bucket_dtype = bucket_dtype
         self._ids = {id(a) for a in self.arenas}
         self._done = {id(a): [] for a in self.arenas}
         self._works = []
@@ -51,13 +61,33 @@ class GradBucketReducer:
         return self._comm
 
     def _issue(self, t):
+        lib = CM.is_lib(self.group)
+        half = self.bucket_dtype == torch.bfloat16
         if t.is_cuda:
             comm = self._comm_stream(t.device)
             comm.wait_stream(torch.cuda.current_stream(t.device))
             with torch.cuda.stream(comm):
-                self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+                b = t.to(torch.bfloat16) if half else t
+                if lib:  # enqueued on the comm stream itself: ordered before the cast back and finish()'s wait
+                    self.group.all_reduce_(b, stream=comm)
+                    w = None
+                else:
+                    w = dist.all_reduce(b, group=self.group, async_op=True)
+                if half:
+                    if w is not None:
+                        w.wait()  # the comm stream waits for the collective before the cast back
+                        w = None
+                    t.copy_(b)
+                self._works.append(w if w is not None else _StreamDone(comm))
         else:
-            self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+            if lib:
+                raise ValueError("a clipmi Communicator reduces device tensors")
+            b = t.to(torch.bfloat16) if half else t
+            w = dist.all_reduce(b, group=self.group, async_op=not half)
+            if half:
+                t.copy_(b)
+            else:
+                self._works.append(w)
 
     def ready(self, arena, off, n):
         if id(arena) not in self._ids or n <= 0:
@@ -91,6 +121,18 @@ class GradBucketReducer:
         self._works = []
 
 
+class _StreamDone:
+    """A bucket enqueued on the communication stream: waiting means the caller's stream waits for that stream."""
+
+    def __init__(self, stream):
+        self.dev = stream.device
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def wait(self):
+        torch.cuda.current_stream(self.dev).wait_event(self.ev)
+
+
 class FusedAdamW:
     """torch.optim.AdamW semantics (decoupled weight decay, bias-corrected) over arenas.
 
@@ -98,7 +140,7 @@ class FusedAdamW:
     trainable parameter's slice gets its own launch of the same kernel."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, arenas=(),
-                 process_group=None):
+                 process_group=None, grad_bucket_dtype=torch.float32):
         params = list(params)
         if not params:
             raise ValueError("optimizer got an empty parameter list")
@@ -130,8 +172,8 @@ class FusedAdamW:
         self._gn = (ctypes.c_int64 * n)()
         self._norm_ws = torch.empty(int(_lib.lib().clipmi_grad_norm_multi_ws(n)), dtype=torch.uint8, device=dev)
         self.reducer = None
-        if process_group is not None and (dist.get_world_size(process_group) > 1 or T.force_collectives()):
-            self.reducer = GradBucketReducer(self.arenas, process_group)
+        if process_group is not None and (CM.world_rank(process_group)[0] > 1 or T.force_collectives()):
+            self.reducer = GradBucketReducer(self.arenas, process_group, grad_bucket_dtype)
 
     def overlap_with(self, model):
         """Let ``armed_backward`` report the model's gradient buckets to this optimizer's reducer."""
@@ -165,7 +207,7 @@ class FusedAdamW:
             self.reducer.finish()
             return
         for a in self.arenas:
-            dist.all_reduce(a.grad, group=group)
+            CM.all_reduce_(a.grad, group)
 
     def clip_grad_norm(self, max_norm):
         """norm over all trainable gradients -> self.norm = [total_norm, clip_coef] on device."""
@@ -227,7 +269,9 @@ class CLIPAdapterTrainer:
     def _world(self):
         if self.process_group is None and not (dist.is_available() and dist.is_initialized()):
             return 1
-        return dist.get_world_size(self.process_group)
+        if self.process_group is None:
+            return dist.get_world_size()
+        return CM.world_rank(self.process_group)[0]
 
     def train_step(self, batch, step, total_steps):
         """One reference step (trainer.py:81-99); returns the loss tensor (no host sync)."""

@@ -146,12 +146,17 @@ extern "C" int clipmi_reducescatter_grad(void* stream, void* comm, int dtype, co
 }
 
 extern "C" int clipmi_allreduce_grads(void* stream, void* comm, float* grads, int64_t count) {
-  CLIPMI_REQUIRE(comm && count >= 0, "allreduce_grads: args");
+  return clipmi_allreduce(stream, comm, CLIPMI_F32, grads, count);
+}
+
+// in-place sum over the ranks of an fp32 or bf16 buffer (bf16: the optional half-size gradient buckets)
+extern "C" int clipmi_allreduce(void* stream, void* comm, int dtype, void* buf, int64_t count) {
+  CLIPMI_REQUIRE(comm && count >= 0 && (dtype == CLIPMI_F32 || dtype == CLIPMI_BF16), "allreduce: args");
   if (count == 0) return CLIPMI_OK;
-  CLIPMI_REQUIRE(grads, "allreduce_grads: buffer");
+  CLIPMI_REQUIRE(buf, "allreduce: buffer");
   const Rccl& r = rccl();
   CLIPMI_RCCL(r);
-  const int e = r.all_reduce(grads, grads, (size_t)count, kF32, kSum, (Comm)comm, (hipStream_t)stream);
+  const int e = r.all_reduce(buf, buf, (size_t)count, dtype_code(dtype), kSum, (Comm)comm, (hipStream_t)stream);
   if (e) return rccl_fail(r, e, "ncclAllReduce");
   return CLIPMI_OK;
 }

@@ -209,6 +209,28 @@ int gemm8(void* s, int M, int N, int K, const void* A, int64_t lda, const void* 
   return gemm8q(s, M, N, K, q8, s8, Wq, Ws, C, ldc, flags, bias, res, ldr);
 }
 
+// Deferred-reduction hazard check: a recorded second stage (DeferredReduce) reads its split-K slabs /
+// bias partials or LayerNorm partial rows when the next persistent GEMM hosts it, so no launch queued in between
+// may write those bytes.  Today's order never does (the two slab regions alternate, ln_guard runs an outstanding
+// affine sum before the next LayerNorm backward); this check makes a future reordering or a new launch that breaks
+// it fail with CLIPMI_ERR_INVALID instead of silently corrupting a gradient.  Host pointer arithmetic only.
+bool overlaps(const void* a, int64_t na, const void* b, int64_t nb) {
+  const char* pa = (const char*)a;
+  const char* pb = (const char*)b;
+  return a && b && na > 0 && nb > 0 && pa < pb + nb && pb < pa + na;
+}
+int pending_hazard(const DeferredReduce& r, const void* dst, int64_t bytes, const char* what) {
+  bool hit = false;
+  if (r.kind == 1) {
+    hit = overlaps(dst, bytes, r.ws, (int64_t)r.splits * r.M * r.N * 4) ||
+          overlaps(dst, bytes, r.bws, (int64_t)r.splits * r.M * 4);
+  } else if (r.kind == 2) {
+    hit = overlaps(dst, bytes, r.part, (int64_t)r.P * r.stride * 4);
+  }
+  if (hit) return clipmi_invalid(std::string("encoder_bwd: ") + what + " would overwrite the inputs of a deferred reduction");
+  return CLIPMI_OK;
+}
+
 int validate(const clipmi_encoder_desc* d) {
   CLIPMI_REQUIRE(d && d->layers && d->act, "null descriptor");
   CLIPMI_REQUIRE(d->dtype == CLIPMI_BF16 || d->dtype == CLIPMI_F32 || d->dtype == CLIPMI_FP8, "dtype");
@@ -349,6 +371,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     // an outstanding split-K sum still reading this region runs first (not reached with the alternation)
     if (pend.kind == 1 && (const char*)pend.ws >= wsl && (const char*)pend.ws < wsl + region)
       CLIPMI_TRY(launch_deferred((hipStream_t)s, pend));
+    CLIPMI_TRY(pending_hazard(pend, wsl, region, "a weight gradient's split-K slabs"));
     CLIPMI_TRY(gemm(s, dt, M, N, R, A, lda, false, B, ldb, false, C, N, f32, CLIPMI_EPI_BETA, nullptr, nullptr, 0,
                     nullptr, 0, sp, wsl, region, fuse ? bgrad : nullptr));
     if (!fuse) CLIPMI_TRY(clipmi_colsum(s, dt, A, lda, R, M, bgrad, 1, wcol, col_bytes));
@@ -357,8 +380,19 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   // LayerNorm backward rewrites the partial rows an outstanding affine sum reads: run that one first
   auto ln_guard = [&]() -> int {
     if (pend.kind == 2) CLIPMI_TRY(launch_deferred((hipStream_t)s, pend));
-    return CLIPMI_OK;
+    return pending_hazard(pend, wln, ln_bytes, "a LayerNorm backward's partial rows");
   };
+  // the activation-gradient buffers every other launch of the loop writes (dbig, dln, g2, and the caller's dx) must
+  // lie outside the regions a deferred reduction reads (the split-K slabs, the LayerNorm partial rows)
+  {
+    const int64_t es_ = (int64_t)esize(dt);
+    const void* dst[4] = {dbig, dln, g2, dx};
+    const int64_t nb[4] = {(int64_t)R * std::max(3 * D, F) * es_, (int64_t)R * D * es_, (int64_t)R * D * es_,
+                           (int64_t)R * D * es_};
+    for (int i = 0; i < 4; ++i)
+      CLIPMI_REQUIRE(!overlaps(dst[i], nb[i], wsplit, split_bytes) && !overlaps(dst[i], nb[i], wln, ln_bytes),
+                     "an activation-gradient buffer overlaps the deferred reductions' slabs / partial rows");
+  }
   for (int l = layer_hi - 1; l >= layer_lo; --l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
