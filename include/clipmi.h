@@ -230,6 +230,20 @@ int clipmi_attention_fwd_mxfp8(void* stream, const void* qkv, uint8_t* o8, uint8
                                const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 int clipmi_attention_bwd(void* stream, int dtype, const void* qkv, const void* o, const float* lse, const void* dout,
                          void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
+/* bf16x3 split images (the layout of CLIPMI_GEMM_SPLIT3's operands): clipmi_split3 writes the image of an fp32
+   operand -- k-major X [rows][K] -> bf16 [rows][3K], else X [K][rows] -> [3K][round8(rows)] -- with segments
+   (h, h, l) for pattern 0 or (h, l, h) for pattern 1, h = bf16(x), l = bf16(x - h); clipmi_split3_elems gives its
+   size in elements.  clipmi_split3_colsum writes the k-major image of x [R, N] and, with colsum, adds x's column
+   sums to colsum[N] (+= when beta; ws >= clipmi_split3_colsum_ws(R, N) bytes, 16-byte aligned). */
+int64_t clipmi_split3_elems(int rows, int K, int kmajor);
+int clipmi_split3(void* stream, const float* X, int64_t ldx, int rows, int K, int kmajor, void* out, int pattern);
+int64_t clipmi_split3_colsum_ws(int R, int N);
+int clipmi_split3_colsum(void* stream, const float* x, int64_t ldx, int R, int N, void* out, int pattern,
+                         float* colsum, int beta, void* ws, int64_t ws_bytes);
+/* LayerNorm of fp32 x with fp32 affine weights written as the bf16x3 split image y3 [R][3D] of its output
+   (pattern as above); mean / rstd saved as in clipmi_layernorm_fwd.  D / 64 in {1, 2, 3, 4, 6, 8, 12, 16}. */
+int clipmi_layernorm_fwd_x3(void* stream, const float* x, int64_t ldx, void* y3, int pattern, const float* w,
+                            const float* b, float* mean, float* rstd, int R, int D, float eps);
 /* The bf16x3 precision mode's attention (csrc/attention_x3.hip): fp32 operands and outputs exactly as
    clipmi_attention_fwd / _bwd with dtype CLIPMI_F32, every product (q k^T, P v, dO v^T, dS k, dS^T q, P^T dO)
    run as three bf16 MFMA products of the hi / lo operand splits (~2^-16 relative per product).  N > 288 falls
@@ -274,10 +288,14 @@ typedef struct clipmi_encoder_desc {
    * operand stays bf16.  The reference is fp32 end to end (trainer.py:81-99); rounding the residual sum
    * to bf16 at each of the 2L residual adds was the largest bf16-mode error (profiles/r05_bf16_error_sources.log). */
   int resid_f32;
-  /* dtype CLIPMI_F32 only (precision "bf16x3"): every GEMM of the forward and backward runs as a
-   * split-operand bf16 product (CLIPMI_GEMM_SPLIT3) with its split images in x3_ws (x3_ws_bytes >=
-   * clipmi_encoder_x3_ws, 256-byte aligned; one scratch per concurrently running encoder); activations,
-   * LayerNorm, attention and gradients stay fp32. */
+  /* dtype CLIPMI_F32 only (precision "bf16x3"): every GEMM of the forward and backward runs as three bf16
+   * products of hi / lo operand splits, over split images (clipmi_split3) that each activation's and activation
+   * gradient's producer writes once; attention as clipmi_attention_fwd_x3 / _bwd_x3; LayerNorm, softmax,
+   * residual stream and all accumulation fp32.  Scratch in x3_ws (x3_ws_bytes >= clipmi_encoder_x3_ws, 256-byte
+   * aligned; one scratch per concurrently running encoder).  The saved activations change form in this mode:
+   * act[l].ln1 / .ln2 hold the bf16 [R][3D] images of the LayerNorm outputs, act[l].o the fp32 [R][D] attention
+   * output followed (at the next 256-byte boundary) by its [R][3D] image, act[l].act the bf16 [R][3F] image of
+   * fc1's output; x_in, qkv, h and pre stay fp32 (csrc/engine.cpp encoder_fwd_x3). */
   int gemm_x3;
   void* x3_ws;
   int64_t x3_ws_bytes;

@@ -729,3 +729,68 @@ def test_layernorm_bwd_any_width_lds_grows():
         xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
         F.layer_norm(xr, (D,), wr, br, 1e-5).backward(dy)
         assert rel(dx, xr.grad) < 1e-4 and rel(dw, wr.grad) < 1e-4 and rel(db, br.grad) < 1e-4, D
+
+
+def _split_ref(x, pattern):
+    """bf16x3 image of fp32 x [R, N]: [R, 3N] bf16, segments (h, h, l) (pattern 0) or (h, l, h) (pattern 1)."""
+    h = x.to(torch.bfloat16)
+    lo = (x - h.float()).to(torch.bfloat16)
+    return torch.cat([h, h, lo] if pattern == 0 else [h, lo, h], dim=1)
+
+
+@pytest.mark.parametrize("R,N", [(1000, 768), (77, 512), (5, 2304), (3, 3072)])
+@pytest.mark.parametrize("pattern", [0, 1])
+def test_split3_colsum_and_layernorm_x3(R, N, pattern):
+    """The bf16x3 mode's producers: clipmi_split3_colsum writes the split image bit for bit (h = bf16(x),
+    l = bf16(x - h)) and adds the column sums (the bias gradient) onto colsum; clipmi_layernorm_fwd_x3 writes the
+    image of the fp32 LayerNorm output (== clipmi_layernorm_fwd's fp32 output, split)."""
+    x = rnd((R, N), 7, torch.float32)
+    out = torch.empty(R, 3 * N, dtype=torch.bfloat16, device="cuda")
+    cs0 = rnd((N,), 8, torch.float32)
+    cs = cs0.clone()
+    ws = T._ws(T._lib.lib().clipmi_split3_colsum_ws(R, N), "cuda")
+    s = kern.stream()
+    T.call("clipmi_split3_colsum", s, x.data_ptr(), N, R, N, out.data_ptr(), pattern, cs.data_ptr(), 1,
+           ws.data_ptr(), ws.numel())
+    assert torch.equal(out, _split_ref(x, pattern))
+    assert rel(cs - cs0, x.double().sum(0)) < 1e-5
+    if N % 64 == 0 and N // 64 in (1, 2, 3, 4, 6, 8, 12, 16):
+        w = rnd((N,), 9, torch.float32) * 0.2 + 1
+        b = rnd((N,), 10, torch.float32) * 0.1
+        y = torch.empty(R, N, device="cuda")
+        st = torch.empty(2, R, device="cuda")
+        T.call("clipmi_layernorm_fwd", s, F32, x.data_ptr(), N, y.data_ptr(), N, w.data_ptr(), b.data_ptr(),
+               st[0].data_ptr(), st[1].data_ptr(), R, N, 1e-5, None, None, 0)
+        y3 = torch.empty(R, 3 * N, dtype=torch.bfloat16, device="cuda")
+        st3 = torch.empty(2, R, device="cuda")
+        T.call("clipmi_layernorm_fwd_x3", s, x.data_ptr(), N, y3.data_ptr(), pattern, w.data_ptr(), b.data_ptr(),
+               st3[0].data_ptr(), st3[1].data_ptr(), R, N, 1e-5)
+        assert torch.equal(y3, _split_ref(y, pattern)) and torch.equal(st, st3)
+
+
+def test_gemm_over_split_images_matches_split3_flag():
+    """A bf16 GEMM over pre-split images (the engine's bf16x3 path since round 6) -- forward (k-major images,
+    reduction 3K) and weight gradient (images read as [3R][K], reduction over 3R interleaved rows) -- against
+    the CLIPMI_GEMM_SPLIT3 flag's split-per-call product and fp64."""
+    from clipmi import _lib
+    R, K, N = 600, 256, 384
+    x = rnd((R, K), 21, torch.float32)
+    w = rnd((N, K), 22, torch.float32) * 0.05
+    s = kern.stream()
+    x3 = torch.empty(R, 3 * K, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, x.data_ptr(), K, R, K, 1, x3.data_ptr(), 0)
+    assert torch.equal(x3, _split_ref(x, 0))
+    w3 = torch.empty(N, 3 * K, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, w.data_ptr(), K, N, K, 1, w3.data_ptr(), 1)
+    y = torch.empty(R, N, device="cuda")
+    kern.gemm(R, N, 3 * K, x3, 3 * K, True, w3, 3 * K, True, y, N)
+    y_flag = torch.empty(R, N, device="cuda")
+    kern.gemm(R, N, K, x, K, True, w, K, True, y_flag, N, split3=True)
+    ref = x.double() @ w.double().T
+    assert rel(y, ref) < 1e-4 and rel(y, y_flag) < 1e-5
+    # weight gradient: gW[N][K] = sum_r dy[r][n] x[r][k] from a pattern-1 image of dy and the pattern-0 image of x
+    dy = rnd((R, N), 23, torch.float32)
+    dy3 = _split_ref(dy, 1).contiguous()
+    gw = torch.zeros(N, K, device="cuda")
+    kern.gemm(N, K, 3 * R, dy3, N, False, x3, K, False, gw, K, flags=_lib.EPI_BETA)
+    assert rel(gw, dy.double().T @ x.double()) < 1e-4

@@ -139,6 +139,12 @@ _lib.declare("clipmi_scatter_rows", [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_in
 _lib.declare("clipmi_attention_fwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd", [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_int])
+_lib.declare("clipmi_split3_elems", [c_int, c_int, c_int], c_i64)
+_lib.declare("clipmi_split3", [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int])
+_lib.declare("clipmi_split3_colsum_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_split3_colsum", [c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_i64])
+_lib.declare("clipmi_layernorm_fwd_x3", [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                                         ctypes.c_float])
 _lib.declare("clipmi_attention_fwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_fwd_mxfp8", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
@@ -224,16 +230,21 @@ class Encoder:
     def grads(self):
         return self._table(LayerG, self.arena.grad)
 
-    def alloc(self, B, N, dtype, device, train, resid32=False):
+    def alloc(self, B, N, dtype, device, train, resid32=False, x3=False):
         """Activation storage: per-layer for training, one shared set for inference.  resid32: the
-        residual stream (x_in, h) in fp32 (the bf16 mode's fp32 residual stream)."""
+        residual stream (x_in, h) in fp32 (the bf16 mode's fp32 residual stream).  x3 (the bf16x3 mode, fp32):
+        ln1 / ln2 / act as bf16 split images [R, 3K] and o followed by its image (include/clipmi.h gemm_x3)."""
         t = self.t
         R, D, F, H, L = B * N, t.hidden_size, t.intermediate_size, t.num_attention_heads, t.num_hidden_layers
         es = 2 if dtype == torch.bfloat16 else 4
         xs = 4 if resid32 else es
         al = lambda n: (n + 255) // 256 * 256  # noqa: E731
-        parts = [("x_in", R * D * xs), ("ln1", R * D * es), ("qkv", R * 3 * D * es), ("o", R * D * es),
-                 ("h", R * D * xs), ("ln2", R * D * es), ("act", R * F * es),
+        x3 = x3 and dtype == torch.float32
+        ln_b = R * 3 * D * 2 if x3 else R * D * es
+        o_b = al(R * D * 4) + R * 3 * D * 2 if x3 else R * D * es
+        act_b = R * 3 * F * 2 if x3 else R * F * es
+        parts = [("x_in", R * D * xs), ("ln1", ln_b), ("qkv", R * 3 * D * es), ("o", o_b),
+                 ("h", R * D * xs), ("ln2", ln_b), ("act", act_b),
                  ("mean1", R * 4), ("rstd1", R * 4), ("lse", B * H * N * 4), ("mean2", R * 4), ("rstd2", R * 4)]
         if train:
             parts.append(("pre", R * F * es))
@@ -399,7 +410,7 @@ class VisionTowerFn(torch.autograd.Function):
             Wp = torch.nn.functional.pad(Wp, (0, Kp - Kc))
         x3 = getattr(rt, "x3", False)  # bf16x3 mode: the patch product split too
         K.gemm(R, D, Kp, X, Kp, True, Wp, Kp, True, h0, D, split3=x3)
-        buf, acts = rt.venc.alloc(B, N, dtype, dev, train, resid32=r32)
+        buf, acts = rt.venc.alloc(B, N, dtype, dev, train, resid32=r32, x3=x3)
         stats0 = torch.empty(2, R, dtype=torch.float32, device=dev)
         call("clipmi_layernorm_fwd", s, dcode(xdtype), P_(h0), D, acts[0].x_in, D,
              arena.ptr("vision_model.pre_layrnorm.weight", ebuf), arena.ptr("vision_model.pre_layrnorm.bias", ebuf),
@@ -504,7 +515,7 @@ class TextTowerFn(torch.autograd.Function):
         fp8 = rt.fp8 and not train
         r32 = getattr(rt, "resid32", False) and not fp8  # the fp32 residual stream (bf16 mode)
         xdtype = torch.float32 if r32 else dtype
-        buf, acts = rt.tenc.alloc(B, S, dtype, dev, train, resid32=r32)
+        buf, acts = rt.tenc.alloc(B, S, dtype, dev, train, resid32=r32, x3=getattr(rt, "x3", False))
         bad = rt.bad_flag
         ebuf = arena.data if r32 else wbuf  # fp32 token / position embeddings into the fp32 stream
         call("clipmi_text_embed", s, dcode(xdtype), P_(ids), arena.ptr("text_model.embeddings.token_embedding.weight", ebuf),

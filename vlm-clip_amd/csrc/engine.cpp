@@ -48,30 +48,10 @@ namespace {
 size_t esize(int dt) { return dt == CLIPMI_F32 ? 4 : 2; }
 int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-// The bf16x3 mode's split-image scratch of the encoder call in progress on this thread (the engine only
-// enqueues work, so a call's GEMMs are issued by the calling thread between X3Scope's bounds).
-struct X3 {
-  void* ws;
-  int64_t bytes;
-};
-thread_local const X3* t_x3 = nullptr;
-struct X3Scope {
-  X3 x3;
-  explicit X3Scope(const clipmi_encoder_desc* d) : x3{d->x3_ws, d->x3_ws_bytes} {
-    t_x3 = (d->gemm_x3 && d->dtype == CLIPMI_F32) ? &x3 : nullptr;
-  }
-  ~X3Scope() { t_x3 = nullptr; }
-};
-
 int gemm(void* s, int dt, int M, int N, int K, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb,
          bool bkm, void* C, int64_t ldc, int c_dt, int flags, const void* bias = nullptr, const void* res = nullptr,
          int64_t ldr = 0, void* aux = nullptr, int64_t ldaux = 0, int split = 1, void* ws = nullptr,
          int64_t ws_bytes = 0, float* bias_grad = nullptr) {
-  if (t_x3 && dt == CLIPMI_F32) {  // bf16x3: the split images (and any split-K slabs) in the x3 scratch
-    flags |= CLIPMI_GEMM_SPLIT3;
-    ws = t_x3->ws;
-    ws_bytes = t_x3->bytes;
-  }
   clipmi_gemm_desc d;
   memset(&d, 0, sizeof(d));
   d.M = M; d.N = N; d.K = K;
@@ -135,25 +115,79 @@ int wgrad_splits(int M, int N, int K, int dt) {
   return best;
 }
 
-// split-K factor of a wgrad GEMM in the encoder's mode (bf16x3: the bf16 kernel over 3R)
-int wgrad_splits_mode(const clipmi_encoder_desc* d, int M, int N, int R) {
-  if (d->gemm_x3 && d->dtype == CLIPMI_F32) return wgrad_splits(M, N, 3 * R, CLIPMI_BF16);
-  return wgrad_splits(M, N, R, d->dtype);
-}
-
-// bf16x3 scratch: the largest split-image set (+ split-K slabs) over the encoder's GEMMs
-int64_t x3_bytes(const clipmi_encoder_desc* d) {
-  if (!d->gemm_x3 || d->dtype != CLIPMI_F32) return 0;
-  const int R = d->B * d->N, D = d->D, F = d->F;
-  int64_t b = 0;
-  const int fw[4][2] = {{3 * D, D}, {D, D}, {F, D}, {D, F}};  // forward [N, K] (both operands k-major)
-  for (auto& f : fw) {
-    b = std::max(b, clipmi_gemm_split3_ws(R, f[0], f[1], 1, 1, 1));
-    b = std::max(b, clipmi_gemm_split3_ws(R, f[1], f[0], 1, 0, 1));  // the input gradient of the same layer
+// ---- bf16x3 mode (fp32 encoder, every GEMM three bf16 products of hi / lo operand splits).  Round 6: the
+// activations and activation gradients are split ONCE, by their producer, into images that serve every GEMM
+// that reads them, instead of once per GEMM operand:
+//   image of X [R][K] (fp32): bf16 [R][3K], segments (h, h, l) ("pattern 0", forward activations) or (h, l, h)
+//   ("pattern 1", activation gradients), h = bf16(X), l = bf16(X - h) -- gemm.hip CLIPMI_GEMM_SPLIT3's layout.
+//   As a k-major operand it is the 3K-long reduction A3 = [Xh | Xh | Xl]; read as [3R][K] with ld = K (row
+//   3r + j = segment j of row r) it is the 3R-long reduction of a weight gradient, where a pattern-1 gradient
+//   image against a pattern-0 activation image pairs (h, h), (l, h), (h, l) row by row: the same three products.
+//   Weights are split per GEMM (pattern 1 against forward activations, pattern 0 against gradients).
+// Producers: LayerNorm writes ln1 / ln2 as images (clipmi_layernorm_fwd_x3); the attention output, fc1's output
+// and the four activation gradients are split by clipmi_split3_colsum, which also sums the gradient's columns
+// into its Linear's bias gradient.  Per layer 6 split passes (round 5: 24, one per GEMM operand).
+// act[l] in this mode: ln1 / ln2 bf16 [R][3D] images; o fp32 [R][D] followed (256-B aligned) by its image; act
+// the bf16 [R][3F] image of fc1's output; x_in, qkv, h, pre (quick_gelu') fp32.
+struct X3Plan {
+  int64_t img, w, slab, col, total;
+};
+X3Plan x3_plan(const clipmi_encoder_desc* d) {
+  const int64_t R = (int64_t)d->B * d->N, D = d->D, F = d->F;
+  X3Plan p;
+  p.img = 0;  // the live activation-gradient image, or fc1's fp32 output in the forward
+  p.w = p.img + align256(std::max(R * 3 * std::max(F, 3 * D) * 2, R * F * 4));
+  int64_t wmax = 0;  // weight images: forward k-major [N][3K], input gradient [3N][round8(K)]
+  const int ws_[4][2] = {{3 * (int)D, (int)D}, {(int)D, (int)D}, {(int)F, (int)D}, {(int)D, (int)F}};
+  for (auto& w : ws_) {
+    wmax = std::max(wmax, clipmi_split3_elems(w[0], w[1], 1));
+    wmax = std::max(wmax, clipmi_split3_elems(w[1], w[0], 0));
   }
-  const int wg[4][2] = {{D, F}, {F, D}, {D, D}, {3 * D, D}};
-  for (auto& w : wg) b = std::max(b, clipmi_gemm_split3_ws(w[0], w[1], R, 0, 0, wgrad_splits_mode(d, w[0], w[1], R)));
-  return b;
+  p.slab = p.w + align256(wmax * 2);
+  int64_t smax = 0;
+  const int wg[4][2] = {{(int)D, (int)F}, {(int)F, (int)D}, {(int)D, (int)D}, {3 * (int)D, (int)D}};
+  for (auto& w : wg) {
+    const int sp = wgrad_splits(w[0], w[1], (int)(3 * R), CLIPMI_BF16);
+    if (sp > 1) smax = std::max(smax, (int64_t)sp * w[0] * w[1] * 4);
+  }
+  p.col = p.slab + align256(smax);
+  p.total = p.col + align256(clipmi_split3_colsum_ws((int)R, (int)std::max(3 * D, F)));
+  return p;
+}
+bool x3_mode(const clipmi_encoder_desc* d) { return d->gemm_x3 && d->dtype == CLIPMI_F32; }
+int64_t x3_bytes(const clipmi_encoder_desc* d) { return x3_mode(d) ? x3_plan(d).total : 0; }
+// the attention output's image, after its fp32 copy in act[l].o
+void* x3_o3(const clipmi_layer_act& a, int64_t R, int D) { return (char*)a.o + align256(R * D * 4); }
+
+// bf16 GEMM over split images, fp32 C / bias / residual / aux
+int x3_gemm(void* s, int M, int N, int K3, const void* A, int64_t lda, bool akm, const void* B, int64_t ldb, bool bkm,
+            void* C, int64_t ldc, int flags, const void* bias = nullptr, const void* res = nullptr, int64_t ldr = 0,
+            void* aux = nullptr, int64_t ldaux = 0, int split = 1, void* ws = nullptr, int64_t ws_bytes = 0) {
+  clipmi_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.M = M; g.N = N; g.K = K3;
+  g.A = A; g.lda = lda; g.a_kmajor = akm;
+  g.B = B; g.ldb = ldb; g.b_kmajor = bkm;
+  g.C = C; g.ldc = ldc;
+  g.bias = bias; g.residual = res; g.ldr = ldr; g.aux = aux; g.ldaux = ldaux;
+  g.alpha = 1.f; g.flags = flags;
+  g.ab_dtype = CLIPMI_BF16; g.c_dtype = CLIPMI_F32; g.bias_dtype = CLIPMI_F32;
+  g.split_k = split; g.workspace = ws; g.workspace_bytes = ws_bytes;
+  return clipmi_gemm(s, &g);
+}
+// C[R][N] = epi(X3 W^T): X3 the pattern-0 image [R][3K] of the forward activation, W fp32 [N][K]
+int x3_fwd(void* s, char* wimg, int R, int N, int K, const void* X3, const void* W, void* C, int64_t ldc, int flags,
+           const void* bias, const void* res = nullptr, int64_t ldr = 0, void* aux = nullptr, int64_t ldaux = 0) {
+  CLIPMI_TRY(clipmi_split3(s, (const float*)W, K, N, K, 1, wimg, 1));
+  return x3_gemm(s, R, N, 3 * K, X3, 3 * (int64_t)K, true, wimg, 3 * (int64_t)K, true, C, ldc, flags, bias, res, ldr,
+                 aux, ldaux);
+}
+// C[R][Kin] = epi(G3 W): G3 the pattern-1 image [R][3 Nout] of an output gradient, W fp32 [Nout][Kin]
+int x3_dgrad(void* s, char* wimg, int R, int Kin, int Nout, const void* G3, const void* W, void* C, int64_t ldc,
+             int flags, void* aux = nullptr, int64_t ldaux = 0) {
+  CLIPMI_TRY(clipmi_split3(s, (const float*)W, Kin, Kin, Nout, 0, wimg, 0));
+  return x3_gemm(s, R, Kin, 3 * Nout, G3, 3 * (int64_t)Nout, true, wimg, (Kin + 7) / 8 * 8, false, C, ldc, flags,
+                 nullptr, nullptr, 0, aux, ldaux);
 }
 
 struct WsPlan {
@@ -245,6 +279,89 @@ int validate(const clipmi_encoder_desc* d) {
   return CLIPMI_OK;
 }
 
+int encoder_fwd_x3(void* s, const clipmi_encoder_desc* d) {
+  const int R = d->B * d->N, D = d->D, F = d->F;
+  const X3Plan pl = x3_plan(d);
+  char* ws = (char*)d->x3_ws;
+  char* wimg = ws + pl.w;
+  float* fc1o = (float*)(ws + pl.img);  // fc1's fp32 output before its split
+  for (int l = 0; l < d->L; ++l) {
+    const clipmi_layer_w& w = d->layers[l];
+    const clipmi_layer_act& a = d->act[l];
+    void* x_out = (l + 1 < d->L) ? d->act[l + 1].x_in : d->x_out;
+    void* o3 = x3_o3(a, R, D);
+    CLIPMI_TRY(clipmi_layernorm_fwd_x3(s, (const float*)a.x_in, D, a.ln1, 0, (const float*)w.ln1_w,
+                                       (const float*)w.ln1_b, a.mean1, a.rstd1, R, D, d->eps));
+    CLIPMI_TRY(x3_fwd(s, wimg, R, 3 * D, D, a.ln1, w.qkv_w, a.qkv, 3 * D, CLIPMI_EPI_BIAS, w.qkv_b));
+    CLIPMI_TRY(clipmi_attention_fwd_x3(s, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)a.o, D, R, D, o3, 0, nullptr, 0, nullptr, 0));
+    CLIPMI_TRY(x3_fwd(s, wimg, R, D, D, o3, w.out_w, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b, a.x_in, D));
+    CLIPMI_TRY(clipmi_layernorm_fwd_x3(s, (const float*)a.h, D, a.ln2, 0, (const float*)w.ln2_w,
+                                       (const float*)w.ln2_b, a.mean2, a.rstd2, R, D, d->eps));
+    const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_DACT : 0);
+    CLIPMI_TRY(x3_fwd(s, wimg, R, F, D, a.ln2, w.fc1_w, fc1o, F, f1, w.fc1_b, nullptr, 0, a.pre, F));
+    CLIPMI_TRY(clipmi_split3_colsum(s, fc1o, F, R, F, a.act, 0, nullptr, 0, nullptr, 0));
+    CLIPMI_TRY(x3_fwd(s, wimg, R, D, F, a.act, w.fc2_w, x_out, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.fc2_b, a.h, D));
+  }
+  return CLIPMI_OK;
+}
+
+int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi, int layer_lo) {
+  const int R = d->B * d->N, D = d->D, F = d->F;
+  const WsPlan p = plan(d);
+  CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= p.total, "encoder_bwd workspace too small");
+  char* bws = (char*)d->workspace;
+  float* g2 = (float*)(bws + p.g2);
+  float* dln = (float*)(bws + p.dln);
+  float* dbig = (float*)(bws + p.dbig);
+  void* wln = bws + p.ln;
+  const int64_t ln_bytes = p.total - p.ln;
+  const X3Plan pl = x3_plan(d);
+  char* ws = (char*)d->x3_ws;
+  void* gimg = ws + pl.img;  // the live activation-gradient image
+  char* wimg = ws + pl.w;
+  void* slab = ws + pl.slab;
+  void* col = ws + pl.col;
+  const int64_t slab_bytes = pl.col - pl.slab, col_bytes = pl.total - pl.col;
+  // gradient image of G [R][N] (pattern 1) into gimg, its column sums added to the bias gradient
+  auto split_g = [&](const float* G, int N, float* bgrad) -> int {
+    return clipmi_split3_colsum(s, G, N, R, N, gimg, 1, bgrad, 1, col, col_bytes);
+  };
+  // C[M][N] += sum over the 3R interleaved rows of G3^T X3 (G3: gradient image, X3: activation image)
+  auto wgrad = [&](int M, int N, const void* G3, const void* X3, float* C) -> int {
+    const int sp = wgrad_splits(M, N, 3 * R, CLIPMI_BF16);
+    return x3_gemm(s, M, N, 3 * R, G3, M, false, X3, N, false, C, N, CLIPMI_EPI_BETA, nullptr, nullptr, 0, nullptr, 0,
+                   sp, sp > 1 ? slab : nullptr, sp > 1 ? slab_bytes : 0);
+  };
+  for (int l = layer_hi - 1; l >= layer_lo; --l) {
+    const clipmi_layer_w& w = d->layers[l];
+    const clipmi_layer_act& a = d->act[l];
+    const clipmi_layer_grad& g = d->grads[l];
+    CLIPMI_REQUIRE(a.pre, "training forward must save pre-activations");
+    // MLP branch: dx is dL/dy
+    CLIPMI_TRY(split_g((const float*)dx, D, g.fc2_b));                                      // gb2 += sum dx
+    CLIPMI_TRY(x3_dgrad(s, wimg, R, F, D, gimg, w.fc2_w, dbig, F, CLIPMI_EPI_MUL_AUX, a.pre, F));  // d_pre
+    CLIPMI_TRY(wgrad(D, F, gimg, a.act, g.fc2_w));                                          // gW2 += dx^T act
+    CLIPMI_TRY(split_g(dbig, F, g.fc1_b));                                                  // gb1 += sum d_pre
+    CLIPMI_TRY(wgrad(F, D, gimg, a.ln2, g.fc1_w));                                          // gW1 += d_pre^T ln2
+    CLIPMI_TRY(x3_dgrad(s, wimg, R, D, F, gimg, w.fc1_w, dln, D, 0));                       // d_ln2 = d_pre W1
+    CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx,
+                                     D, g.ln2_w, g.ln2_b, 1, wln, ln_bytes, R, D));          // dh = dx + LN2'(d_ln2)
+    // attention branch: g2 is dL/dh
+    CLIPMI_TRY(split_g(g2, D, g.out_b));                                                    // gbo += sum dh
+    CLIPMI_TRY(x3_dgrad(s, wimg, R, D, D, gimg, w.out_w, dln, D, 0));                       // d_o = dh Wo
+    CLIPMI_TRY(wgrad(D, D, gimg, x3_o3(a, R, D), g.out_w));                                 // gWo += dh^T o
+    CLIPMI_TRY(clipmi_attention_bwd_x3(s, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                       d->N, D));                                           // d_qkv
+    CLIPMI_TRY(split_g(dbig, 3 * D, g.qkv_b));                                              // gbqkv += sum d_qkv
+    CLIPMI_TRY(wgrad(3 * D, D, gimg, a.ln1, g.qkv_w));                                      // gWqkv += d_qkv^T ln1
+    CLIPMI_TRY(x3_dgrad(s, wimg, R, D, 3 * D, gimg, w.qkv_w, dln, D, 0));                   // d_ln1
+    CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D,
+                                     g2, D, g.ln1_w, g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
+  }
+  return CLIPMI_OK;
+}
+
 }  // namespace
 
 extern "C" int64_t clipmi_encoder_bwd_ws(const clipmi_encoder_desc* d) { return plan(d).total; }
@@ -255,7 +372,7 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
   const int dt = d->dtype;
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
-  X3Scope x3(d);
+  if (x3_mode(d)) return encoder_fwd_x3(s, d);
   if (dt == CLIPMI_FP8) {  // BASELINE config 5: frozen towers, MXFP8 GEMMs, bf16 everything else
     const int bf = CLIPMI_BF16;
     // scratch: [R, D] operand (LayerNorm / attention outputs) then [R, F] (fc1 output), each with its scales
@@ -299,10 +416,7 @@ extern "C" int clipmi_encoder_fwd(void* s, const clipmi_encoder_desc* d) {
     CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.x_in, D, a.ln1, D, w.ln1_w, w.ln1_b, a.mean1, a.rstd1, R, D, d->eps,
                                      nullptr, nullptr, 0));
     CLIPMI_TRY(gemm(s, dt, R, 3 * D, D, a.ln1, D, true, w.qkv_w, D, true, a.qkv, 3 * D, dt, CLIPMI_EPI_BIAS, w.qkv_b));
-    if (t_x3)  // bf16x3: the attention products split too
-      CLIPMI_TRY(clipmi_attention_fwd_x3(s, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
-    else
-      CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    CLIPMI_TRY(clipmi_attention_fwd(s, dt, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
     CLIPMI_TRY(gemm(s, dt, R, D, D, a.o, D, true, w.out_w, D, true, a.h, D, xdt, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID,
                     w.out_b, a.x_in, D));
     CLIPMI_TRY(clipmi_layernorm_fwd2(s, xdt, dt, a.h, D, a.ln2, D, w.ln2_w, w.ln2_b, a.mean2, a.rstd2, R, D, d->eps,
@@ -335,9 +449,9 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   const int xdt = (dt == CLIPMI_BF16 && d->resid_f32) ? CLIPMI_F32 : dt;  // the saved x_in / h
   const int R = d->B * d->N, D = d->D, F = d->F;
   if (R == 0) return CLIPMI_OK;
+  if (x3_mode(d)) return encoder_bwd_x3(s, d, dx, layer_hi, layer_lo);
   const WsPlan p = plan(d);
   CLIPMI_REQUIRE(d->workspace && d->workspace_bytes >= p.total, "encoder_bwd workspace too small");
-  X3Scope x3(d);
   char* ws = (char*)d->workspace;
   void* g2 = ws + p.g2;
   void* dln = ws + p.dln;
@@ -365,7 +479,7 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
   // gradient (sum_tokens A[t][m]) into the same GEMM, fp32 uses a column-sum pass
   auto wgrad = [&](int M, int N, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                    float* bgrad) -> int {
-    const int sp = wgrad_splits_mode(d, M, N, R);
+    const int sp = wgrad_splits(M, N, R, d->dtype);
     const bool fuse = dt == CLIPMI_BF16;
     char* wsl = (char*)wsplit + (dt == CLIPMI_BF16 ? (wg_no++ & 1) * region : 0);
     // an outstanding split-K sum still reading this region runs first (not reached with the alternation)
@@ -410,12 +524,8 @@ extern "C" int clipmi_encoder_bwd_layers(void* s, const clipmi_encoder_desc* d, 
     // attention branch: g2 is dL/dh
     CLIPMI_TRY(gemm(s, dt, R, D, D, g2, D, true, w.out_w, D, false, dln, D, dt, 0));     // d_o = dh Wo
     CLIPMI_TRY(wgrad(D, D, g2, D, a.o, D, g.out_w, g.out_b));                            // gWo += dh^T o
-    if (t_x3)
-      CLIPMI_TRY(clipmi_attention_bwd_x3(s, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
-                                         d->N, D));                         // d_qkv
-    else
-      CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
-                                      d->N, D));                            // d_qkv
+    CLIPMI_TRY(clipmi_attention_bwd(s, dt, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                    d->N, D));                              // d_qkv
     CLIPMI_TRY(wgrad(3 * D, D, dbig, 3 * D, a.ln1, D, g.qkv_w, g.qkv_b));  // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(gemm(s, dt, R, D, 3 * D, dbig, 3 * D, true, w.qkv_w, D, false, dln, D, dt, 0));  // d_ln1
     CLIPMI_TRY(ln_guard());

@@ -1492,6 +1492,15 @@ int gemm_split3(hipStream_t s, const clipmi_gemm_desc* d) {
 }
 }  // namespace
 
+// The split image of one fp32 operand (CLIPMI_GEMM_SPLIT3's layout): k-major X [rows][K] -> [rows][3K], else X [K][rows]
+// -> [3K][round8(rows)]; pattern 0: segments (h, h, l), 1: (h, l, h).  out: clipmi_split3_elems(rows, K, kmajor) bf16.
+extern "C" int64_t clipmi_split3_elems(int rows, int K, int kmajor) { return split3_elems(rows, K, kmajor != 0); }
+extern "C" int clipmi_split3(void* stream, const float* X, int64_t ldx, int rows, int K, int kmajor, void* out,
+                             int pattern) {
+  CLIPMI_REQUIRE(X && out && rows >= 0 && K >= 0 && (pattern == 0 || pattern == 1), "split3: arguments");
+  return split3_operand((hipStream_t)stream, X, ldx, rows, K, kmajor != 0, (bf16*)out, pattern);
+}
+
 extern "C" int64_t clipmi_gemm_split3_ws(int M, int N, int K, int a_kmajor, int b_kmajor, int split_k) {
   if (M < 0 || N < 0 || K < 0) return 0;
   int64_t b = al256b(split3_elems(M, K, a_kmajor) * 2) + al256b(split3_elems(N, K, b_kmajor) * 2);

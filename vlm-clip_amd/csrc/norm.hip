@@ -53,7 +53,10 @@ constexpr int LN_RPW = 2;
 // Q8: y is written as MXFP8 instead (q8 [R, D] e4m3 bytes, s8 [R, D/32] E8M0): a 32-element
 // block is 8 consecutive lanes' 4-element pieces (PS == 4), max-reduced across those lanes; the
 // fp8 operand of the next GEMM without a bf16 round trip through HBM.
-template <typename TX, typename T, int PS, int NP, bool Q8 = false>
+// X3 (bf16x3 mode, fp32 x / w / b): y is written as the split image of the next GEMM's operand instead --
+// bf16 [R][3D] (ldy = 3D), segments (h, h, l) for X3 = 1 or (h, l, h) for X3 = 2 with h = bf16(y), l = bf16(y - h)
+// (gemm.hip CLIPMI_GEMM_SPLIT3's layout), so no fp32 copy and no split pass between the LayerNorm and its GEMMs.
+template <typename TX, typename T, int PS, int NP, bool Q8 = false, int X3 = 0>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(TX* x, int64_t ldx, T* y, int64_t ldy, const T* w, const T* b,
                                                      float* mean_out, float* rstd_out, int R, int D, float eps,
                                                      const TX* pos, const TX* cls, int period, uint8_t* q8 = nullptr,
@@ -125,6 +128,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TX* x, int64_t ldx, T* y, i
         const float inv = ldexpf(1.0f, -ex);
         *(uint32_t*)(q8 + (int64_t)(row0 + rr) * D + c) = mx_pack4(o[0], o[1], o[2], o[3], inv);
         if ((lane & 7) == 0) s8[(int64_t)(row0 + rr) * (D >> 5) + (c >> 5)] = (uint8_t)(ex + 127);
+      } else if constexpr (X3 != 0) {
+        float hv[PS], lv[PS];
+#pragma unroll
+        for (int j = 0; j < PS; ++j) {
+          hv[j] = (float)(bf16)o[j];
+          lv[j] = o[j] - hv[j];
+        }
+        bf16* y3 = (bf16*)y + (int64_t)(row0 + rr) * ldy + c;
+        vstore<bf16, PS>(y3, hv);
+        vstore<bf16, PS>(y3 + D, X3 == 1 ? hv : lv);
+        vstore<bf16, PS>(y3 + 2 * D, X3 == 1 ? lv : hv);
       } else {
         vstore<T, PS>(y + (int64_t)(row0 + rr) * ldy + c, o);
       }
@@ -425,6 +439,41 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* x, int64_t
   }
   store4(ws + (int64_t)blockIdx.y * N + c, s);
 }
+// bf16x3 split image of an fp32 [R, N] matrix (k-major [R][3N], segments (h, h, l) for pattern 0 or (h, l, h) for
+// pattern 1) and, when ws, its column partial sums ws[chunk][N] in the same pass (the bias gradient of the GEMM the
+// matrix is the output gradient of); four rows in flight per thread
+__global__ __launch_bounds__(256) void split3_colsum_kernel(const float* x, int64_t ldx, int R, int N, int rows_per,
+                                                            bf16* out, int pattern, float* ws) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ld3 = 3 * (int64_t)N;
+  auto one = [&](int r, const f32x4& v) {
+    bf16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      h[j] = (bf16)v[j];
+      l[j] = (bf16)(v[j] - (float)h[j]);
+      s[j] += v[j];
+    }
+    bf16* o = out + (int64_t)r * ld3 + c;
+    *(bf16x4*)o = h;
+    *(bf16x4*)(o + N) = pattern ? l : h;
+    *(bf16x4*)(o + 2 * N) = pattern ? h : l;
+  };
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const f32x4*)(x + (int64_t)(r + u) * ldx + c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(r + u, v[u]);
+  }
+  for (; r < r1; ++r) one(r, *(const f32x4*)(x + (int64_t)r * ldx + c));
+  if (ws) store4(ws + (int64_t)blockIdx.y * N + c, s);
+}
+
 // the same, one column per thread: any N, ldx and alignment (fp32 adapters of any bottleneck width)
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_partial1_kernel(const T* x, int64_t ldx, int R, int N, int rows_per,
@@ -607,6 +656,19 @@ void ln_fwd_launch(hipStream_t s, void* x, int64_t ldx, void* y, int64_t ldy, co
                      (T*)y, ldy, (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const TX*)pos, (const TX*)cls, period);
 }
 template <typename TX, typename T, int PS, int NP>
+void ln_fwd_x3_launch(hipStream_t s, void* x, int64_t ldx, void* y3, int pattern, const void* w, const void* b,
+                      float* mean, float* rstd, int R, int D, float eps) {
+  const dim3 g((R + 4 * LN_RPW - 1) / (4 * LN_RPW));
+  if (pattern == 0)
+    hipLaunchKernelGGL((ln_fwd_kernel<TX, T, PS, NP, false, 1>), g, dim3(256), 0, s, (TX*)x, ldx, (T*)y3, (int64_t)3 * D,
+                       (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const TX*)nullptr, (const TX*)nullptr, 1,
+                       (uint8_t*)nullptr, (uint8_t*)nullptr);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<TX, T, PS, NP, false, 2>), g, dim3(256), 0, s, (TX*)x, ldx, (T*)y3, (int64_t)3 * D,
+                       (const T*)w, (const T*)b, mean, rstd, R, D, eps, (const TX*)nullptr, (const TX*)nullptr, 1,
+                       (uint8_t*)nullptr, (uint8_t*)nullptr);
+}
+template <typename TX, typename T, int PS, int NP>
 void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t* s8, const void* w, const void* b,
                       float* mean, float* rstd, int R, int D, float eps) {
   if constexpr (PS == 4) {
@@ -707,6 +769,18 @@ extern "C" int clipmi_layernorm_fwd(void* stream, int dtype, void* x, int64_t ld
                                     const void* w, const void* b, float* mean, float* rstd, int R, int D,
                                     float eps, const void* pos, const void* cls, int period) {
   return clipmi_layernorm_fwd2(stream, dtype, dtype, x, ldx, y, ldy, w, b, mean, rstd, R, D, eps, pos, cls, period);
+}
+
+// fp32 x / weights -> the bf16x3 split image [R][3D] of y (pattern 0: segments h, h, l; 1: h, l, h)
+extern "C" int clipmi_layernorm_fwd_x3(void* stream, const float* x, int64_t ldx, void* y3, int pattern, const float* w,
+                                       const float* b, float* mean, float* rstd, int R, int D, float eps) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(ln_fast_width(D), "layernorm_fwd_x3: D / 64 must be one of 1, 2, 3, 4, 6, 8, 12, 16");
+  CLIPMI_REQUIRE(x && y3 && w && b && (pattern == 0 || pattern == 1), "layernorm_fwd_x3: arguments");
+  if (R == 0) return CLIPMI_OK;
+  LN_DISPATCH(D, ln_fwd_x3_launch, float, float, s, (void*)x, ldx, y3, pattern, w, b, mean, rstd, R, D, eps);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
 }
 
 extern "C" int clipmi_layernorm_fwd_mxfp8(void* stream, int dtype, const void* x, int64_t ldx, uint8_t* q8,
@@ -819,6 +893,37 @@ extern "C" int64_t clipmi_colsum_ws(int R, int N) {
   if (chunks > 512) chunks = 512;
   if (chunks < 1) chunks = 1;
   return (int64_t)chunks * N * 4;
+}
+
+extern "C" int64_t clipmi_split3_colsum_ws(int R, int N) {
+  int chunks = (R + 127) / 128;
+  if (chunks > 1024) chunks = 1024;
+  if (chunks < 1) chunks = 1;
+  return (int64_t)chunks * N * 4;
+}
+
+// bf16x3 mode: the split image out [R][3N] (pattern 0: h, h, l; 1: h, l, h) of x [R, N] fp32, and with colsum its
+// column sums added to colsum[N] (+= when beta) -- the bias gradient read in the same pass
+extern "C" int clipmi_split3_colsum(void* stream, const float* x, int64_t ldx, int R, int N, void* out, int pattern,
+                                    float* colsum, int beta, void* ws, int64_t ws_bytes) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(x && out && (pattern == 0 || pattern == 1) && R >= 0, "split3_colsum: arguments");
+  CLIPMI_REQUIRE(N % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 7) == 0,
+                 "split3_colsum: N, ldx multiples of 4, x 16-byte and out 8-byte aligned");
+  int chunks = (R + 127) / 128;
+  if (chunks > 1024) chunks = 1024;
+  if (chunks < 1) chunks = 1;
+  CLIPMI_REQUIRE(!colsum || (ws && ws_bytes >= (int64_t)chunks * N * 4 && ((uintptr_t)ws & 15) == 0),
+                 "split3_colsum: workspace (clipmi_split3_colsum_ws, 16-byte aligned)");
+  if (R == 0 || N == 0) return CLIPMI_OK;
+  const int rows_per = (R + chunks - 1) / chunks;
+  hipLaunchKernelGGL(split3_colsum_kernel, dim3((N / 4 + 255) / 256, chunks), dim3(256), 0, s, x, ldx, R, N, rows_per,
+                     (bf16*)out, pattern, colsum ? (float*)ws : nullptr);
+  if (colsum)
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, (const float*)ws, (int64_t)N,
+                       chunks, N, colsum, (float*)nullptr, beta);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
 }
 
 // out[n] (+)= sum_r x[r][n]   (bias gradients)
