@@ -24,8 +24,13 @@ def test_single_rank_collectives_exact(dtype):
         c.all_reduce_(g)
         torch.cuda.synchronize()
         assert torch.equal(g, g0)
+        gb = g.to(torch.bfloat16)  # the bf16 gradient buckets (clipmi_allreduce with CLIPMI_BF16)
+        gb0 = gb.clone()
+        c.all_reduce_(gb)
+        torch.cuda.synchronize()
+        assert torch.equal(gb, gb0)
         with pytest.raises(ValueError):
-            c.all_reduce_(x.to(torch.bfloat16))
+            c.all_reduce_(x.to(torch.float16))
     finally:
         c.close()
 
