@@ -1237,7 +1237,7 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
   // residual fused; the patch embedding; the bf16x3 split products): the same kernels, fp32 epilogue
   if (f32o && !p.ws && splits == 1 && sel == 3) {
     if ((w4_default || p.var == 28) && (flags == E_B || flags == (E_B | E_R) || flags == 0)) {
-      if (const char* l = dispatch_w4_f32(p, s, flags)) return l;
+      if (const char* l = dispatch_w4_f32(p, s, flags, true)) return l;
     }
     switch (flags) {
       case E_B: launch256<true, true, float, E_B, false>(p, splits, s, bg); return "gemm256_fwd_bias_f32";
@@ -1249,8 +1249,12 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
       default: break;
     }
   }
-  // the bf16x3 mode's input gradients (fp32 gradients; fc2's with the stored-derivative product)
+  // the bf16x3 mode's input gradients (fp32 gradients; fc2's with the stored-derivative product); the plain
+  // ones (K' = 3K >= 2304) on the persistent 4-wave kernel, whose long-K main loop is the faster one
   if (f32o && !p.ws && splits == 1 && sel == 2) {
+    if ((w4_default || p.var == 28) && flags == 0) {
+      if (const char* l = dispatch_w4_f32(p, s, flags, false)) return l;
+    }
     switch (flags) {
       case 0: launch256<true, false, float, 0, false>(p, splits, s, bg); return "gemm256_dgrad_f32";
       case E_MA: launch256<true, false, float, E_MA, false>(p, splits, s, bg); return "gemm256_dgrad_mulaux_f32";

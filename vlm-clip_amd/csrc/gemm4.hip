@@ -1018,8 +1018,13 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
 
 // fp32-output forward products (k-major B) on the persistent kernel: the bf16 mode's fp32 residual stream
 // (fc2 with bias + residual) and fp32-output bf16 products
-const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags) {
+const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags, bool bkm) {
   constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID;
+  if (!bkm) {  // the bf16x3 mode's plain input gradients (K' = 3K >= 2304), fp32 out
+    if (flags != 0) return nullptr;
+    launch_w4p<true, false, float, 0, false>(p, 1, s, nullptr);
+    return "gemm256_dgrad_f32";
+  }
   switch (flags) {
     case E_B | E_R: launch_w4p<true, true, float, E_B | E_R, false>(p, 1, s, nullptr); return "gemm256_fwd_bias_resid_f32";
     case E_B: launch_w4p<true, true, float, E_B, false>(p, 1, s, nullptr); return "gemm256_fwd_bias_f32";

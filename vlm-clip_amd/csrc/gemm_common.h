@@ -909,7 +909,7 @@ __device__ __forceinline__ void epilogue_q8(const GemmP& p, f32x4 (&acc)[NI][4],
 // 4-wave 256x256 kernel (gemm4.hip) for the forward / dgrad layouts; nullptr if not covered
 const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int dm);
 // its fp32-output forward form (flags bias, bias + residual, none); nullptr if not covered
-const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags);
+const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags, bool bkm);
 // its persistent weight-gradient form (both operands row-major in k, fp32 out, split-K slabs)
 const char* dispatch_w4_wgrad(const GemmP& p, int splits, hipStream_t s, int flags, float* bg);
 // its MXFP8 form (gemm4.hip gemm_w4p8_kernel); nullptr if the shape or epilogue is not covered
