@@ -1,8 +1,8 @@
 """End-to-end parity of clipmi.CLIPWithAdapters / CLIPAdapterTrainer on the GPU against
 goldens produced by running the reference (tests/golden, tools/gen_goldens.py) and the
 CPU oracle.  Tolerances: fp32 parity mode -> logits within 1e-3 absolute (north_star);
-bf16 MFMA mode -> logits within 0.15 absolute at logit scale 100 (bf16 GEMMs over
-12-24 layers; SURVEY §6 measured 0.058-0.146 for bf16 variants of the reference itself)."""
+bf16 MFMA mode -> logits within 0.07 absolute at logit scale 100 (bf16 GEMM operands over
+12-24 layers, fp32 residual stream; SURVEY §6 measured 0.058-0.146 for bf16 variants of the reference itself)."""
 import hashlib
 
 import numpy as np
@@ -15,10 +15,12 @@ from clipmi import CLIPWithAdapters, CLIPAdapterTrainer, synth  # noqa: E402
 from clipmi import config as C  # noqa: E402
 
 # bf16x3: fp32 activations, tower GEMMs as bf16x3 split products -- held to the fp32 tolerances
-LOGIT_TOL = {"fp32": 1e-3, "bf16x3": 1e-3, "bf16": 0.15}
+# bf16 (fp32 residual stream, trained and frozen towers since round 6): measured 0.019-0.033 on the full-size
+# fixtures (B/32, B/16, L/14, L/14@336; round 5 with the bf16 stream on frozen towers 0.042-0.12), bound ~2x that
+LOGIT_TOL = {"fp32": 1e-3, "bf16x3": 1e-3, "bf16": 0.07}
 # the tiny 2-layer fixture has 64-dim features: bf16 rounding of LN'd activations is ~1 %
-# per element there, so its bf16 logits get a looser bound than the full-size models
-BF16_TINY_LOGIT_TOL = 0.35
+# per element there, so its bf16 logits get a looser bound than the full-size models (measured 0.122)
+BF16_TINY_LOGIT_TOL = 0.25
 
 
 def batch(cfg, B, g=None, seed=1234):
@@ -64,9 +66,8 @@ def test_forward_matches_reference(golden, precision, tag, preset, B, adapters):
 
 @pytest.mark.parametrize("tag,preset,B,adapters", [("b32", "B/32", 8, True), ("l14", "L/14", 2, True)])
 def test_frozen_towers_fp32_residual_forward(golden, tag, preset, B, adapters):
-    """residual_fp32=True on frozen towers (the default only when the towers are trained): the bf16 mode
-    with the fp32 residual stream against the reference goldens, at a tighter bound than the bf16-residual
-    forward's 0.15."""
+    """residual_fp32=True given explicitly on frozen towers (the default since round 6; round 5 kept the bf16 stream
+    there): the bf16 mode with the fp32 residual stream against the reference goldens."""
     g = golden(f"forward_{tag}.npz")
     m = CLIPWithAdapters(preset, use_text_adapter=adapters, use_vision_adapter=adapters, use_shared_adapters=False,
                          freeze_clip=True, device="cuda", precision="bf16", residual_fp32=True)
