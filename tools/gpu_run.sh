@@ -38,7 +38,7 @@ for step in "$@"; do
     attn) run 300 $log python tools/attn_bench.py ${arg//,/ } ;;
     fp8) run 600 $log python tools/fp8_bench.py ${arg//,/ } ;;
     prof) run 600 $log rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o b16 -- \
-            python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-sample 0 ${arg//,/ } ;;
+            python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-sample 0 --parity-steps 0 ${arg//,/ } ;;
     pmc) run 600 $log bash tools/${arg%%:*} $(echo ${arg#*:} | tr , ' ') ;;
     py) f=${arg%%:*}; a=${arg#*:}; [ "$a" = "$arg" ] && a=""; run 600 $log python $f ${a//,/ } ;;
     smoke) run 300 $log python -c "import __graft_entry__ as g; g.smoke()" ;;
