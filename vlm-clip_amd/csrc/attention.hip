@@ -583,6 +583,18 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_stream(AttnP p) {
 //            dQ (each wave owns 16 queries, K/V images).
 // So every byte the next phase needs is in flight during the current one.  Barriers that
 // must not wait for those plain loads are raw s_barrier (lgkmcnt only).
+// CLIPMI_ATTN_PRIO (A/B builds): raise the wave's issue priority over its MFMA clusters so a SIMD's other wave's
+// exponentials issue beside them instead of competing for issue slots while the matrix pipe waits
+#ifndef CLIPMI_ATTN_PRIO
+#define CLIPMI_ATTN_PRIO 0
+#endif
+__device__ __forceinline__ void prio_hi() {
+  if constexpr (CLIPMI_ATTN_PRIO) __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void prio_lo() {
+  if constexpr (CLIPMI_ATTN_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 __device__ __forceinline__ void raw_barrier_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -644,11 +656,13 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
           sc = f32x4{s0, s0, s0, s0};
           dp = f32x4{-d4[0], -d4[1], -d4[2], -d4[3]};
         }
+        prio_hi();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kf[u][kk], sc, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[kk], vf[u][kk], dp, 0, 0, 0);
         }
+        prio_lo();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if constexpr (!CAUSAL) {
@@ -671,6 +685,7 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
       pf[u] = pack8(pt[u][0], pt[u][1]);
       sf[u] = pack8(ds[u][0], ds[u][1]);
     }
+    prio_hi();
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const bf16x8 td = frag_tr(c.dOimg, qs * 32, v * 16, lane), tq = frag_tr(c.Qimg, qs * 32, v * 16, lane);
@@ -680,6 +695,7 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx& c, const bf16x8 (&kf)[
         dk[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tq, sf[u], dk[u][v], 0, 0, 0);
       }
     }
+    prio_lo();
   }
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
@@ -739,11 +755,13 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
       for (int u = 0; u < NB; ++u) {
         f32x4 sc = seed, dp = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (!CAUSAL) dp = f32x4{-dl[u], -dl[u], -dl[u], -dl[u]};
+        prio_hi();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[kk], qf[u][kk], sc, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[kk], of[u][kk], dp, 0, 0, 0);
         }
+        prio_lo();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if constexpr (!CAUSAL) {
@@ -760,6 +778,7 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
     bf16x8 sf[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) sf[u] = pack8(ds[u][0], ds[u][1]);
+    prio_hi();
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const bf16x8 tk = frag_tr(c.Kimg, ks * 32, v * 16, lane);
@@ -767,6 +786,7 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx& c, const bf16x8 (&qf)[
       for (int u = 0; u < NB; ++u)
         dq[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tk, sf[u], dq[u][v], 0, 0, 0);
     }
+    prio_lo();
   }
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
