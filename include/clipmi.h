@@ -240,6 +240,17 @@ int clipmi_split3(void* stream, const float* X, int64_t ldx, int rows, int K, in
 int64_t clipmi_split3_colsum_ws(int R, int N);
 int clipmi_split3_colsum(void* stream, const float* x, int64_t ldx, int R, int N, void* out, int pattern,
                          float* colsum, int beta, void* ws, int64_t ws_bytes);
+/* A bf16 GEMM (d->ab_dtype CLIPMI_BF16, d->c_dtype CLIPMI_F32: the epilogue computes in fp32) whose result is
+   written as its split image instead -- d->C bf16 [M][d->ldc], ldc >= 3N, segments at columns n, N + n, 2N + n in
+   the pattern above -- by the producing kernel's epilogue (the bf16x3 mode's fc1 output and fc2 input gradient,
+   which clipmi_split3_colsum would otherwise split from an fp32 copy).  Flags: bias + quick_gelu (+ store_dact:
+   the derivative to fp32 aux), or mul_aux (fp32 aux).  colsum (+= when beta): the column sums of the fp32 result,
+   ws >= clipmi_gemm_x3out_ws(M, N) bytes, 256-byte aligned.  clipmi_gemm_x3out_ok: whether a shape / layout /
+   flag set has this form (k-major A, M >= 256, N >= 128, N % 8 == 0, K % 64 == 0). */
+int64_t clipmi_gemm_x3out_ws(int M, int N);
+int clipmi_gemm_x3out_ok(int M, int N, int K, int a_kmajor, int b_kmajor, int flags);
+int clipmi_gemm_x3out(void* stream, const clipmi_gemm_desc* d, int pattern, float* colsum, int beta, void* ws,
+                      int64_t ws_bytes);
 /* LayerNorm of fp32 x with fp32 affine weights written as the bf16x3 split image y3 [R][3D] of its output
    (pattern as above); mean / rstd saved as in clipmi_layernorm_fwd.  D / 64 in {1, 2, 3, 4, 6, 8, 12, 16}. */
 int clipmi_layernorm_fwd_x3(void* stream, const float* x, int64_t ldx, void* y3, int pattern, const float* w,

@@ -768,6 +768,74 @@ def test_split3_colsum_and_layernorm_x3(R, N, pattern):
         assert torch.equal(y3, _split_ref(y, pattern)) and torch.equal(st, st3)
 
 
+@pytest.mark.parametrize("R", [600, 520, 777])
+def test_gemm_x3out_writes_the_split_image(R):
+    """clipmi_gemm_x3out (the bf16x3 mode's fc1 forward and fc2 input gradient since round 6): the epilogue writes the
+    split image of its fp32 result instead of the result -- equal to the fp32-output product split afterwards
+    (clipmi_split3_colsum's rounding), with fc1's fp32 derivative beside it and the pattern-1 product's column sums
+    (the bias gradient) added onto colsum.  R = 520 / 777: partial 256-row tiles, one with a wave wholly past M."""
+    from clipmi import _lib
+    K, N = 256, 384
+    s = kern.stream()
+    x = rnd((R, K), 31, torch.float32)
+    w = rnd((N, K), 32, torch.float32) * 0.05
+    b = rnd((N,), 33, torch.float32) * 0.1
+    x3 = torch.empty(R, 3 * K, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, x.data_ptr(), K, R, K, 1, x3.data_ptr(), 0)
+    w3 = torch.empty(N, 3 * K, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, w.data_ptr(), K, N, K, 1, w3.data_ptr(), 1)
+    fl = _lib.EPI_BIAS | _lib.EPI_QGELU | _lib.EPI_STORE_DACT
+    assert T._lib.lib().clipmi_gemm_x3out_ok(R, N, 3 * K, 1, 1, fl)
+    y = torch.empty(R, N, device="cuda")
+    dact = torch.empty(R, N, device="cuda")
+    kern.gemm(R, N, 3 * K, x3, 3 * K, True, w3, 3 * K, True, y, N, bias=b, aux=dact, ldaux=N, flags=fl)
+    img = torch.full((R, 3 * N), float("nan"), dtype=torch.bfloat16, device="cuda")
+    dact2 = torch.empty(R, N, device="cuda")
+    kern.gemm_x3out(R, N, 3 * K, x3, 3 * K, w3, 3 * K, True, img, 0, bias=b, aux=dact2, ldaux=N, flags=fl)
+    ref = _split_ref(y, 0)
+    assert torch.equal(img[:, :N], img[:, N:2 * N])
+    hl = img[:, :N].float() + img[:, 2 * N:].float()
+    # h + l keeps ~16 of fp32's 24 bits (2^-17 relative); the image is bit for bit the split of the fp32 product
+    mh = (img[:, :N] != ref[:, :N]).float().mean().item()
+    ml = (img[:, 2 * N:] != ref[:, 2 * N:]).float().mean().item()
+    print(f"\n[x3out fc1 R={R}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, y) {rel(hl, y):.2e}")
+    assert rel(hl, y) < 2e-5 and torch.equal(img, ref)
+    assert rel(dact2, dact) < 1e-6
+    # fc2's input gradient: d_pre = (dy W2) * dact, pattern 1, bias gradient of fc1 from its column sums
+    dy = rnd((R, K), 34, torch.float32)
+    dy3 = torch.empty(R, 3 * K, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, dy.data_ptr(), K, R, K, 1, dy3.data_ptr(), 1)
+    w2 = rnd((K, N), 35, torch.float32) * 0.05  # fc2 weight [out K][in N]
+    ld8 = (N + 7) // 8 * 8
+    w23 = torch.zeros(3 * K, ld8, dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_split3", s, w2.data_ptr(), N, N, K, 0, w23.data_ptr(), 0)
+    g = torch.empty(R, N, device="cuda")
+    kern.gemm(R, N, 3 * K, dy3, 3 * K, True, w23, ld8, False, g, N, aux=dact, ldaux=N, flags=_lib.EPI_MUL_AUX)
+    assert rel(g, (dy.double() @ w2.double()) * dact.double()) < 1e-4
+    gimg = torch.full((R, 3 * N), float("nan"), dtype=torch.bfloat16, device="cuda")
+    cs0 = rnd((N,), 36, torch.float32)
+    cs = cs0.clone()
+    kern.gemm_x3out(R, N, 3 * K, dy3, 3 * K, w23, ld8, False, gimg, 1, aux=dact, ldaux=N, flags=_lib.EPI_MUL_AUX,
+                    colsum=cs)
+    assert torch.equal(gimg[:, :N], gimg[:, 2 * N:])
+    hl = gimg[:, :N].float() + gimg[:, N:2 * N].float()
+    gref = _split_ref(g, 1)
+    mh = (gimg[:, :N] != gref[:, :N]).float().mean().item()
+    ml = (gimg[:, N:2 * N] != gref[:, N:2 * N]).float().mean().item()
+    print(f"[x3out fc2 dgrad R={R}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, g) {rel(hl, g):.2e}")
+    assert rel(hl, g) < 2e-5 and torch.equal(gimg, gref)
+    assert rel(cs - cs0, g.double().sum(0)) < 1e-5
+    cs1 = torch.zeros(N, device="cuda")
+    kern.gemm_x3out(R, N, 3 * K, dy3, 3 * K, w23, ld8, False, gimg, 1, aux=dact, ldaux=N, flags=_lib.EPI_MUL_AUX,
+                    colsum=cs1, beta=False)
+    assert rel(cs1, g.double().sum(0)) < 1e-5
+    # shapes / flags without the fused form are refused (the engine checks clipmi_gemm_x3out_ok first)
+    assert not T._lib.lib().clipmi_gemm_x3out_ok(200, N, 3 * K, 1, 1, fl)
+    assert not T._lib.lib().clipmi_gemm_x3out_ok(R, N, 3 * K, 1, 1, _lib.EPI_BIAS)
+    with pytest.raises(ValueError, match="x3out"):
+        kern.gemm_x3out(200, N, 3 * K, x3, 3 * K, w3, 3 * K, True, img, 0, bias=b, aux=dact2, ldaux=N, flags=fl)
+
+
 def test_gemm_over_split_images_matches_split3_flag():
     """A bf16 GEMM over pre-split images (the engine's bf16x3 path since round 6) -- forward (k-major images,
     reduction 3K) and weight gradient (images read as [3R][K], reduction over 3R interleaved rows) -- against

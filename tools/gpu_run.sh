@@ -32,7 +32,7 @@ for step in "$@"; do
   name=${step%%=*}; arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
   log=gpurun_out/${TAG}_${i}_${name}.log
   case $name in
-    tests) ta=${arg:-tests}; run 1000 $log python -u -m pytest ${ta//,/ } -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tests) ta=${arg:-tests}; run 1000 $log python -u -m pytest ${ta//,/ } -m gpu -x -q -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) run 600 $log python bench.py ${arg//,/ } ;;
     gemm) GEMM_VARIANTS=${arg%%:*} run 600 $log python tools/gemm_bench.py $(echo ${arg#*:} | tr , ' ') ;;
     attn) run 300 $log python tools/attn_bench.py ${arg//,/ } ;;

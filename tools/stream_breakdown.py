@@ -8,10 +8,10 @@ from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
-main = next(r["Stream_Id"] for r in rows if "attn_fwd_pf<14" in r["Kernel_Name"] or "attn_fwd_pfILi14" in r["Kernel_Name"])
+main = next(r["Stream_Id"] for r in rows if re.search(r"attn_fwd_(pf|x3)(<|ILi)14", r["Kernel_Name"]))
 FAM = [("gemm fwd/dgrad 8-wave", r"gemm_pp_kernel"), ("gemm 4-wave persistent (fwd/dgrad)", r"gemm_w4p_kernel(ILb1|<true)"),
        ("gemm 4-wave persistent (wgrad)", r"gemm_w4p_kernel(ILb0|<false)"), ("gemm wgrad 8-wave", r"gemm256_kernel"),
-       ("split-K reduce", r"splitk_reduce"), ("attention fwd", r"attn_fwd"), ("attention bwd", r"attn_bwd"),
+       ("split-K reduce", r"splitk_reduce"), ("bf16x3 split", r"split3"), ("attention fwd", r"attn_fwd"), ("attention bwd", r"attn_bwd"),
        ("layernorm fwd", r"ln_fwd"), ("layernorm bwd", r"ln_bwd"), ("LN affine-grad reduce", r"reduce_partials"),
        ("adamw / norm", r"adamw|sumsq|grad_norm"), ("embeddings / im2col / pooling", r"im2col|text_embed|id_|period_sum|pool|scatter|gather"),
        ("contrastive", r"ce_|l2norm|gemm_f32|sum2"), ("torch / copies", r"at::native|rocclr")]

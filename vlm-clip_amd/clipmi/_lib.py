@@ -55,6 +55,10 @@ _declare("clipmi_build_digest", ctypes.c_char_p, [])
 _declare("clipmi_last_error", ctypes.c_char_p, [])
 _declare("clipmi_gemm", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc)])
 _declare("clipmi_gemm_split3_ws", ctypes.c_int64, [ctypes.c_int] * 6)
+_declare("clipmi_gemm_x3out_ws", ctypes.c_int64, [ctypes.c_int] * 2)
+_declare("clipmi_gemm_x3out_ok", ctypes.c_int, [ctypes.c_int] * 6)
+_declare("clipmi_gemm_x3out", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc), ctypes.c_int, c_vp, ctypes.c_int, c_vp,
+                                             c_i64])
 _declare("clipmi_gemm_batched", ctypes.c_int, [c_vp, ctypes.POINTER(GemmDesc), ctypes.c_int, ctypes.c_int]
          + [ctypes.c_int64] * 6)
 

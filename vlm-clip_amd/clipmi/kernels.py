@@ -69,6 +69,35 @@ def gemm(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, *, bias=None, resi
     return C
 
 
+def gemm_x3out(M, N, K, A, lda, B, ldb, b_kmajor, C3, pattern, *, bias=None, aux=None, ldaux=0, flags=0,
+               colsum=None, beta=True):
+    """The bf16x3 mode's image-output product (include/clipmi.h clipmi_gemm_x3out): bf16 k-major A, the fp32
+    epilogue's result written as the split image C3 bf16 [M][3N] (pattern 0: h, h, l; 1: h, l, h); colsum (fp32
+    [N]): the result's column sums added (beta) or stored."""
+    _on_gpu(A, B, C3, bias, aux, colsum)
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or C3.dtype != torch.bfloat16:
+        raise ValueError("gemm_x3out: bf16 operands and image")
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = A.data_ptr(), lda, 1
+    d.B, d.ldb, d.b_kmajor = B.data_ptr(), ldb, int(b_kmajor)
+    d.C, d.ldc = C3.data_ptr(), 3 * N
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.aux, d.ldaux = (aux.data_ptr() if aux is not None else None), ldaux
+    d.alpha, d.flags = 1.0, flags
+    d.ab_dtype, d.c_dtype = BF16, F32
+    d.bias_dtype = dt(bias) if bias is not None else F32
+    d.split_k = 1
+    ws = None
+    if colsum is not None:
+        ws = torch.empty(int(_lib.lib().clipmi_gemm_x3out_ws(M, N)), dtype=torch.uint8, device=C3.device)
+    _lib.check(_lib.lib().clipmi_gemm_x3out(stream(), ctypes.byref(d), pattern,
+                                            colsum.data_ptr() if colsum is not None else None, int(beta),
+                                            ws.data_ptr() if ws is not None else None,
+                                            ws.numel() if ws is not None else 0), "clipmi_gemm_x3out")
+    return C3
+
+
 def gemm_batched(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, nb1, nb2, sa, sb, sc, *, alpha=1.0,
                  beta=False):
     """nb1 x nb2 fp32 products in one launch: product (i1, i2) reads A + i1 sa[0] + i2 sa[1], B + ...,

@@ -151,7 +151,8 @@ X3Plan x3_plan(const clipmi_encoder_desc* d) {
     if (sp > 1) smax = std::max(smax, (int64_t)sp * w[0] * w[1] * 4);
   }
   p.col = p.slab + align256(smax);
-  p.total = p.col + align256(clipmi_split3_colsum_ws((int)R, (int)std::max(3 * D, F)));
+  p.total = p.col + align256(std::max(clipmi_split3_colsum_ws((int)R, (int)std::max(3 * D, F)),
+                                      clipmi_gemm_x3out_ws((int)R, (int)F)));
   return p;
 }
 bool x3_mode(const clipmi_encoder_desc* d) { return d->gemm_x3 && d->dtype == CLIPMI_F32; }
@@ -174,6 +175,23 @@ int x3_gemm(void* s, int M, int N, int K3, const void* A, int64_t lda, bool akm,
   g.ab_dtype = CLIPMI_BF16; g.c_dtype = CLIPMI_F32; g.bias_dtype = CLIPMI_F32;
   g.split_k = split; g.workspace = ws; g.workspace_bytes = ws_bytes;
   return clipmi_gemm(s, &g);
+}
+// the same product with its result written as a split image by the GEMM's epilogue (clipmi_gemm_x3out): C3 bf16
+// [M][3N] in pattern `pattern`, colsum (+=) the result's column sums
+int x3_gemm_img(void* s, int M, int N, int K3, const void* A, int64_t lda, const void* B, int64_t ldb, bool bkm,
+                void* C3, int pattern, int flags, const void* bias, void* aux, int64_t ldaux, float* colsum, void* ws,
+                int64_t ws_bytes) {
+  clipmi_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.M = M; g.N = N; g.K = K3;
+  g.A = A; g.lda = lda; g.a_kmajor = 1;
+  g.B = B; g.ldb = ldb; g.b_kmajor = bkm;
+  g.C = C3; g.ldc = 3 * (int64_t)N;
+  g.bias = bias; g.aux = aux; g.ldaux = ldaux;
+  g.alpha = 1.f; g.flags = flags;
+  g.ab_dtype = CLIPMI_BF16; g.c_dtype = CLIPMI_F32; g.bias_dtype = CLIPMI_F32;
+  g.split_k = 1;
+  return clipmi_gemm_x3out(s, &g, pattern, colsum, 1, ws, ws_bytes);
 }
 // C[R][N] = epi(X3 W^T): X3 the pattern-0 image [R][3K] of the forward activation, W fp32 [N][K]
 int x3_fwd(void* s, char* wimg, int R, int N, int K, const void* X3, const void* W, void* C, int64_t ldc, int flags,
@@ -299,8 +317,14 @@ int encoder_fwd_x3(void* s, const clipmi_encoder_desc* d) {
     CLIPMI_TRY(clipmi_layernorm_fwd_x3(s, (const float*)a.h, D, a.ln2, 0, (const float*)w.ln2_w,
                                        (const float*)w.ln2_b, a.mean2, a.rstd2, R, D, d->eps));
     const int f1 = CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU | (a.pre ? CLIPMI_EPI_STORE_DACT : 0);
-    CLIPMI_TRY(x3_fwd(s, wimg, R, F, D, a.ln2, w.fc1_w, fc1o, F, f1, w.fc1_b, nullptr, 0, a.pre, F));
-    CLIPMI_TRY(clipmi_split3_colsum(s, fc1o, F, R, F, a.act, 0, nullptr, 0, nullptr, 0));
+    if (clipmi_gemm_x3out_ok(R, F, 3 * D, 1, 1, f1)) {  // the act image written by fc1's epilogue
+      CLIPMI_TRY(clipmi_split3(s, (const float*)w.fc1_w, D, F, D, 1, wimg, 1));
+      CLIPMI_TRY(x3_gemm_img(s, R, F, 3 * D, a.ln2, 3 * (int64_t)D, wimg, 3 * (int64_t)D, true, a.act, 0, f1, w.fc1_b,
+                             a.pre, F, nullptr, nullptr, 0));
+    } else {
+      CLIPMI_TRY(x3_fwd(s, wimg, R, F, D, a.ln2, w.fc1_w, fc1o, F, f1, w.fc1_b, nullptr, 0, a.pre, F));
+      CLIPMI_TRY(clipmi_split3_colsum(s, fc1o, F, R, F, a.act, 0, nullptr, 0, nullptr, 0));
+    }
     CLIPMI_TRY(x3_fwd(s, wimg, R, D, F, a.act, w.fc2_w, x_out, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.fc2_b, a.h, D));
   }
   return CLIPMI_OK;
@@ -333,16 +357,27 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
     return x3_gemm(s, M, N, 3 * R, G3, M, false, X3, N, false, C, N, CLIPMI_EPI_BETA, nullptr, nullptr, 0, nullptr, 0,
                    sp, sp > 1 ? slab : nullptr, sp > 1 ? slab_bytes : 0);
   };
+  // fc2's input gradient writes d_pre's image itself where the fused form exists (dbig holds dx's image, 6 D B per
+  // row, inside its 4 max(3D, F) B)
+  const bool fuse_dpre = clipmi_gemm_x3out_ok(R, F, 3 * D, 1, 0, CLIPMI_EPI_MUL_AUX) && 3 * D <= 2 * std::max(3 * D, F);
   for (int l = layer_hi - 1; l >= layer_lo; --l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
     const clipmi_layer_grad& g = d->grads[l];
     CLIPMI_REQUIRE(a.pre, "training forward must save pre-activations");
     // MLP branch: dx is dL/dy
-    CLIPMI_TRY(split_g((const float*)dx, D, g.fc2_b));                                      // gb2 += sum dx
-    CLIPMI_TRY(x3_dgrad(s, wimg, R, F, D, gimg, w.fc2_w, dbig, F, CLIPMI_EPI_MUL_AUX, a.pre, F));  // d_pre
-    CLIPMI_TRY(wgrad(D, F, gimg, a.act, g.fc2_w));                                          // gW2 += dx^T act
-    CLIPMI_TRY(split_g(dbig, F, g.fc1_b));                                                  // gb1 += sum d_pre
+    if (fuse_dpre) {  // d_pre's image written by fc2's input-gradient epilogue; dx's image in dbig meanwhile
+      CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)dx, D, R, D, dbig, 1, g.fc2_b, 1, col, col_bytes));  // gb2
+      CLIPMI_TRY(clipmi_split3(s, (const float*)w.fc2_w, F, F, D, 0, wimg, 0));
+      CLIPMI_TRY(x3_gemm_img(s, R, F, 3 * D, dbig, 3 * (int64_t)D, wimg, (F + 7) / 8 * 8, false, gimg, 1,
+                             CLIPMI_EPI_MUL_AUX, nullptr, a.pre, F, g.fc1_b, col, col_bytes));  // d_pre, gb1
+      CLIPMI_TRY(wgrad(D, F, dbig, a.act, g.fc2_w));                                        // gW2 += dx^T act
+    } else {
+      CLIPMI_TRY(split_g((const float*)dx, D, g.fc2_b));                                    // gb2 += sum dx
+      CLIPMI_TRY(x3_dgrad(s, wimg, R, F, D, gimg, w.fc2_w, dbig, F, CLIPMI_EPI_MUL_AUX, a.pre, F));  // d_pre
+      CLIPMI_TRY(wgrad(D, F, gimg, a.act, g.fc2_w));                                        // gW2 += dx^T act
+      CLIPMI_TRY(split_g(dbig, F, g.fc1_b));                                                // gb1 += sum d_pre
+    }
     CLIPMI_TRY(wgrad(F, D, gimg, a.ln2, g.fc1_w));                                          // gW1 += d_pre^T ln2
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, F, gimg, w.fc1_w, dln, D, 0));                       // d_ln2 = d_pre W1
     CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx,

@@ -1512,7 +1512,9 @@ extern "C" int64_t clipmi_gemm_split3_ws(int M, int N, int K, int a_kmajor, int 
   return b;
 }
 
-extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
+namespace {
+// clipmi_gemm with the bf16x3 image output of clipmi_gemm_x3out (x3o 1 / 2: pattern 0 / 1, colp: column partials)
+int gemm_impl(void* stream, const clipmi_gemm_desc* d, int x3o, float* colp) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(d && d->M >= 0 && d->N >= 0 && d->K >= 0, "bad shape");
   // every operand an epilogue flag reads or writes must be given (a null one would fault the GPU)
@@ -1605,6 +1607,8 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   p.bias_f32 = d->bias_dtype == CLIPMI_F32;
   p.ws = nullptr;
   p.bws = nullptr;
+  p.x3o = x3o;
+  p.colp = colp;
   // 256-kernel schedule: the ping-pong kernel for the forward / dgrad layouts, the
   // single-group asm-DMA schedule (var 4) for wgrad, where its 64-k steps measured faster
   // (profiles/r01_gemm_variants*.log).  CLIPMI_GEMM_VAR overrides it for A/B runs.
@@ -1639,6 +1643,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
   const bool kok = (!d->a_kmajor || d->K % 64 == 0) && (!d->b_kmajor || d->K % 64 == 0);
   const bool use256 = bf && kok && ((d->M >= 256 && d->N >= 128) || d->bias_grad) && d->force_small_tile != 1;
   CLIPMI_REQUIRE(!d->bias_grad || use256, "bias_grad fusion needs the 256 kernel (bf16, wgrad layout)");
+  CLIPMI_REQUIRE(!x3o || (use256 && splits == 1), "x3out: needs the 256-tile kernels (M >= 256, N >= 128, K % 64 == 0)");
   const int tile = bf ? (use256 ? BT : BM) : FT;
   const int kstep = bf ? BK : FK;
   if (splits > 1) {
@@ -1674,6 +1679,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
       // tools/gemm_l2_model.py); CLIPMI_RASTER overrides
       if (wlayout && !getenv("CLIPMI_RASTER") && q.tiles_n > q.ntiles / q.tiles_n) q.raster = q.ntiles / q.tiles_n;
       label = dispatch256(q, splits, s, f32o, sel, d->flags, d->bias_grad);
+      CLIPMI_REQUIRE(label || !x3o, "x3out: no image-output kernel for these flags");
     }
     if (!label) {
       CLIPMI_REQUIRE(!d->bias_grad, "bias_grad needs the wgrad layout (both operands row-major in k)");
@@ -1682,6 +1688,7 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
       q.ntiles = q.tiles_n * ((d->M + BM - 1) / BM);
       label = dispatch_bf16(q, splits, s, f32o, sel, d->flags);
     }
+    CLIPMI_REQUIRE(label, "no kernel for this GEMM");
     ps.finish(label, flops);
   } else {
     ProfScope ps(s, nullptr, 0.0);
@@ -1714,6 +1721,79 @@ extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) {
     }
     CLIPMI_CHECK_LAUNCH();
   }
+  return CLIPMI_OK;
+}
+}  // namespace
+
+extern "C" int clipmi_gemm(void* stream, const clipmi_gemm_desc* d) { return gemm_impl(stream, d, 0, nullptr); }
+
+namespace {
+__global__ __launch_bounds__(256) void fold_rows4_kernel(const float* part, int P, int N, int per, float* out) {
+  // out[g][c..c+3] = sum of part rows [g * per, min(P, (g + 1) * per)) in row order; eight rows' loads in flight
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * per, r1 = min(P, r0 + per);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  int r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = *(const f32x4*)(part + (int64_t)(r + j) * N + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  for (; r < r1; ++r) acc += *(const f32x4*)(part + (int64_t)r * N + c);
+  *(f32x4*)(out + (int64_t)blockIdx.y * N + c) = acc;
+}
+constexpr int X3_FOLD = 64;  // first-stage groups of the column sums
+int x3out_parts(int M) { return (M + 127) / 128; }
+}  // namespace
+
+extern "C" int64_t clipmi_gemm_x3out_ws(int M, int N) {
+  if (M <= 0 || N <= 0) return 0;
+  return ((int64_t)x3out_parts(M) * N * 4 + 255) / 256 * 256 + (int64_t)X3_FOLD * N * 4;
+}
+
+extern "C" int clipmi_gemm_x3out_ok(int M, int N, int K, int a_kmajor, int b_kmajor, int flags) {
+  const int x3e = flags & ~CLIPMI_EPI_STORE_DACT;
+  const bool fl = x3e == (CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU) || flags == CLIPMI_EPI_MUL_AUX;
+  return fl && a_kmajor && M >= 256 && N >= 128 && N % 8 == 0 && K % 64 == 0 && (!b_kmajor || K % 64 == 0);
+}
+
+extern "C" int clipmi_gemm_x3out(void* stream, const clipmi_gemm_desc* d, int pattern, float* colsum, int beta,
+                                 void* ws, int64_t ws_bytes) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(d && (pattern == 0 || pattern == 1), "x3out: arguments");
+  CLIPMI_REQUIRE(d->ab_dtype == CLIPMI_BF16 && d->c_dtype == CLIPMI_F32 && d->split_k <= 1 && !d->bias_grad,
+                 "x3out: bf16 operands, fp32 epilogue (c_dtype CLIPMI_F32), no split-K / bias gradient");
+  CLIPMI_REQUIRE(clipmi_gemm_x3out_ok(d->M, d->N, d->K, d->a_kmajor, d->b_kmajor, d->flags),
+                 "x3out: flags bias + quick_gelu (+ store_dact) or mul_aux, k-major A, M >= 256, N >= 128, N % 8 == 0, "
+                 "K % 64 == 0");
+  CLIPMI_REQUIRE(d->C && d->ldc >= 3 * (int64_t)d->N && d->ldc % 8 == 0 && ((uintptr_t)d->C & 15) == 0,
+                 "x3out: C is the bf16 image [M][ldc], ldc >= 3N, ldc % 8 == 0, 16-byte aligned");
+  CLIPMI_REQUIRE(!d->aux || (d->ldaux % 4 == 0 && ((uintptr_t)d->aux & 15) == 0),
+                 "x3out: fp32 aux 16-byte aligned, ldaux % 4 == 0");
+  CLIPMI_REQUIRE(!(d->flags & CLIPMI_EPI_BIAS) || d->bias_dtype == CLIPMI_F32 || ((uintptr_t)d->bias & 15) == 0,
+                 "x3out: bf16 bias 16-byte aligned");
+  float* colp = nullptr;
+  if (colsum) {
+    CLIPMI_REQUIRE(ws && ws_bytes >= clipmi_gemm_x3out_ws(d->M, d->N) && ((uintptr_t)ws & 255) == 0,
+                   "x3out: column-sum workspace (clipmi_gemm_x3out_ws, 256-byte aligned)");
+    colp = (float*)ws;
+  }
+  CLIPMI_TRY(gemm_impl(stream, d, 1 + pattern, colp));
+  if (colsum) {
+    const int P = x3out_parts(d->M);
+    const int per = (P + X3_FOLD - 1) / X3_FOLD, G = (P + per - 1) / per;
+    float* fold = (float*)((char*)ws + ((int64_t)P * d->N * 4 + 255) / 256 * 256);
+    hipLaunchKernelGGL(fold_rows4_kernel, dim3((d->N / 4 + 255) / 256, G), dim3(256), 0, s, colp, P, d->N, per, fold);
+    DeferredReduce r;
+    memset(&r, 0, sizeof(r));
+    r.kind = 2;
+    r.part = fold; r.stride = d->N; r.P = G; r.D = d->N; r.out = colsum; r.out2 = nullptr; r.pbeta = beta;
+    CLIPMI_TRY(launch_partials_reduce(s, r));
+  }
+  CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
 

@@ -37,6 +37,10 @@ struct GemmP {
   int nb2;
   int64_t bsa1, bsa2, bsb1, bsb2, bsc1, bsc2;
   DeferredReduce red;  // persistent 4-wave kernel: a deferred reduction its workgroups run first (kind 0: none)
+  // bf16x3 image output (clipmi_gemm_x3out, fp32-epilogue instances): 0 off, 1 pattern 0 (h, h, l), 2 pattern 1
+  // (h, l, h); colp: per-128-row column partial sums of the fp32 result [ceil(M / 128)][N], or null
+  int x3o;
+  float* colp;
 };
 
 // host side: the stamp buffer armed by clipmi_gemm_stamps (nullptr when disarmed)
@@ -739,6 +743,127 @@ __device__ __forceinline__ void epilogue_lds_pipe(const GemmP& p, f32x4 (&acc)[N
   }
 }
 
+// bf16x3 mode (engine.cpp encoder_*_x3): the fp32 result v of the epilogue leaves as its split image instead of
+// fp32 -- C bf16 [M][ldc], segments at columns n, N + n, 2N + n: (h, h, l) for x3o == 1 (pattern 0, a forward
+// activation) or (h, l, h) for x3o == 2 (pattern 1, an activation gradient), h = bf16(v), l = bf16(v - h): the
+// layout and rounding of clipmi_split3_colsum, so the producer's fp32 copy and the split pass over it disappear.
+// STORE_DACT's derivative stays fp32 (aux), MUL_AUX reads fp32 aux.  With p.colp (pattern 1: the bias gradient of
+// the Linear this is the output gradient of) the column sums of v over the wave's 128 rows go to
+// colp[(mb >> 7) * N + n] (rows in order per lane, then a fixed xor tree over the 16 row lanes: deterministic).
+// Register layout as epilogue256_w: after v_permlane16_swap lane (q, mlane) holds row mb + 16 i + mlane, columns
+// nb + 32 jp + coff .. + 7.  N % 8 == 0, ldc % 8 == 0, C 16-B aligned, aux fp32 16-B aligned (host-checked).
+template <int EPI>
+__device__ __forceinline__ void epilogue_x3img(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
+  // no fma contraction: l = bf16(v - h) of the ROUNDED v (a contracted v * s - h would split the unrounded product
+  // and differ from clipmi_split3_colsum's image of the stored fp32 result in l's last bit for ~1 % of elements)
+#pragma clang fp contract(off)
+  constexpr bool HB = EPI & CLIPMI_EPI_BIAS, HQ = EPI & CLIPMI_EPI_QGELU;
+  constexpr bool HDA = EPI & CLIPMI_EPI_STORE_DACT, HMA = EPI & CLIPMI_EPI_MUL_AUX;
+  const int q = lane >> 4, mlane = lane & 15;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);
+  const int64_t seg = p.N;
+  const bool p1 = p.x3o == 2;
+  float bv[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const int n = min(nb + 32 * jp + coff, p.N - 8);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bv[jp][r] = 0.f;
+    if (HB) {
+      if (p.bias_f32) {
+        load4((const float*)p.bias + n, bv[jp]);
+        load4((const float*)p.bias + n + 4, bv[jp] + 4);
+      } else {
+        load8((const bf16*)p.bias + n, bv[jp]);
+      }
+    }
+  }
+  float cs[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) cs[jp][r] = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float xin[4][2][8];
+    if (HMA) {  // the half's aux rows in one burst (clamped addresses), before its stores
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int m = min(mb + (h * 4 + ii) * 16 + mlane, p.M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const float* a = (const float*)p.aux + (int64_t)m * p.ldaux + min(nb + 32 * jp + coff, p.N - 8);
+          load4(a, xin[ii][jp]);
+          load4(a + 4, xin[ii][jp] + 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = h * 4 + ii;
+      const int m = mb + i * 16 + mlane;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int n = nb + 32 * jp + coff;
+        float v[8], w2[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+          v[r] = __uint_as_float(sw[0]) * p.alpha + bv[jp][r];
+          v[r + 4] = __uint_as_float(sw[1]) * p.alpha + bv[jp][r + 4];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (HQ) {
+            const float sg = qg_sigmoid(v[r]);
+            if (HDA) {  // s + 1.702 x s (1 - s), as epilogue_lds_pipe
+              const float tq = 1.702f * v[r];
+              w2[r] = fmaf(sg, fmaf(-tq, sg, tq), sg);
+            }
+            v[r] *= sg;
+          }
+          if (HMA) v[r] *= xin[ii][jp][r];
+        }
+        if (m < p.M && n < p.N) {
+          if (HDA) {
+            float* a = (float*)p.aux + (int64_t)m * p.ldaux + n;
+            store4(a, w2);
+            store4(a + 4, w2 + 4);
+          }
+          bf16x8 hi, lo;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            hi[r] = (bf16)v[r];
+            lo[r] = (bf16)(v[r] - (float)hi[r]);
+            cs[jp][r] += v[r];
+          }
+          bf16* o = (bf16*)p.C + (int64_t)m * p.ldc + n;
+          *(bf16x8*)o = hi;
+          *(bf16x8*)(o + seg) = p1 ? lo : hi;
+          *(bf16x8*)(o + 2 * seg) = p1 ? hi : lo;
+        }
+      }
+    }
+  }
+  if (p.colp && mb < p.M) {
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) cs[jp][r] += __shfl_xor(cs[jp][r], o, 64);
+      }
+      const int n = nb + 32 * jp + coff;
+      if (mlane == 0 && n < p.N) {
+        float* c = p.colp + (int64_t)(mb >> 7) * p.N + n;
+        store4(c, cs[jp]);
+        store4(c + 4, cs[jp] + 4);
+      }
+    }
+  }
+}
+
 // Store a wave's 128x64 accumulator block: the specialised batched epilogue when the shape
 // allows it (4-aligned columns, aligned leading dims; the 16-B form for bf16 output when
 // columns, leading dims and pointers allow 16-B accesses), else the per-subtile generic path
@@ -748,6 +873,16 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
                                           char* stage = nullptr) {
   constexpr bool FAST = EPI >= 0 && !((EPI & CLIPMI_EPI_RESID) && (EPI & (CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU))) &&
                         !((EPI & CLIPMI_EPI_BETA) && (EPI & (CLIPMI_EPI_RESID | CLIPMI_EPI_DQGELU | CLIPMI_EPI_DGELU)));
+  // bf16x3 image output (clipmi_gemm_x3out): the fp32-output instances of fc1 (bias + quick_gelu, with or
+  // without the stored derivative) and of fc2's input gradient (the stored-derivative product)
+  constexpr int X3E = EPI & ~CLIPMI_EPI_STORE_DACT;
+  if constexpr (std::is_same<OutT, float>::value && !AR &&
+                (X3E == (CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU) || EPI == CLIPMI_EPI_MUL_AUX)) {
+    if (p.x3o) {
+      epilogue_x3img<EPI>(p, acc, mb, nb, lane);
+      return;
+    }
+  }
   // the derivative-store / aux-product flags have a fast form only in the pipelined LDS epilogue
   constexpr bool NEWF = EPI >= 0 && (EPI & (CLIPMI_EPI_STORE_DACT | CLIPMI_EPI_MUL_AUX));
   if constexpr (NEWF) {
