@@ -86,7 +86,9 @@ __device__ __forceinline__ void gfrag_x3(const float* rowbase, int64_t ld, int r
 }
 
 // ------------------------------------------------------------------------------------------- forward
-template <int NKT, bool MASKED>
+// NB query blocks per wave at a time (NB = 2: every K / V fragment read from LDS serves both blocks' products,
+// halving the fragment reads that bound the one-block form -- 2 x NKT x 2 reads of 1 KiB per 16 queries)
+template <int NKT, bool MASKED, int NB>
 __global__ __launch_bounds__(512, 1) void attn_fwd_x3(AttnX p, int causal) {
   constexpr int NPAD = NKT * 16, IMG = NPAD * 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -109,80 +111,104 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_x3(AttnX p, int causal) {
   const int g = lane >> 4, li = lane & 15;
   const float c2 = p.scale * LOG2E;
   const int nqb = (N + 15) >> 4;
-  for (int qb = wave; qb < nqb; qb += 8) {
-    const int q = qb * 16 + li;
-    bf16x8 qh[2], ql[2];
+  for (int qb0 = wave * NB; qb0 < nqb; qb0 += 8 * NB) {
+    int q[NB];
+    bf16x8 qh[NB][2], ql[NB][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) gfrag_x3(base, ld, q, N, kk, g, qh[kk], ql[kk]);
+    for (int j = 0; j < NB; ++j) {
+      q[j] = (qb0 + j) * 16 + li;  // a block past nqb computes on zero rows and stores nothing
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) gfrag_x3(base, ld, q[j], N, kk, g, qh[j][kk], ql[j][kk]);
+    }
     // key-major scores: lane (g, li) holds keys kt * 16 + 4 g + r of query li
-    f32x4 sc[NKT];
+    f32x4 sc[NB][NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        sc[kt] = mfma3(frag_row(Kh, kt * 16 + li, kk * 4 + g), frag_row(Kl, kt * 16 + li, kk * 4 + g), qh[kk], ql[kk],
-                       sc[kt]);
+      for (int j = 0; j < NB; ++j) sc[j][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 fh = frag_row(Kh, kt * 16 + li, kk * 4 + g), fl = frag_row(Kl, kt * 16 + li, kk * 4 + g);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) sc[j][kt] = mfma3(fh, fl, qh[j][kk], ql[j][kk], sc[j][kt]);
+      }
       // one tile's fragment reads in flight at a time: hoisting every tile's K fragments (16 VGPRs each) above
       // the MFMAs spilled from NKT = 10 on
       __builtin_amdgcn_sched_barrier(0);
     }
-    float mx = NEG_INF;
+    float mref[NB], lsum[NB];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
+    for (int j = 0; j < NB; ++j) {
+      float mx = NEG_INF;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        if (MASKED) {
-          if (!(keyok[key] && (!causal || key <= q))) sc[kt][r] = NEG_INF;
-        } else if (kt >= NKT - 2 && key >= N) {  // NPAD = N rounded up to 32: padding in the last two tiles only
-          sc[kt][r] = NEG_INF;
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + 4 * g + r;
+          if (MASKED) {
+            if (!(keyok[key] && (!causal || key <= q[j]))) sc[j][kt][r] = NEG_INF;
+          } else if (kt >= NKT - 2 && key >= N) {  // NPAD = N rounded up to 32: padding in the last two tiles only
+            sc[j][kt][r] = NEG_INF;
+          }
+          mx = fmaxf(mx, sc[j][kt][r]);
         }
-        mx = fmaxf(mx, sc[kt][r]);
       }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mref[j] = mx == NEG_INF ? 0.f : mx * c2;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][r], c2, -mref[j]));
+          sc[j][kt][r] = e;
+          ls += e;
+        }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      lsum[j] = ls;
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mref = mx == NEG_INF ? 0.f : mx * c2;
-    float lsum = 0.f;
+    // O^T = V^T P^T, the P tiles split per 32-key step straight from the score registers
+    f32x4 acc[NB][4];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], c2, -mref));
-        sc[kt][r] = e;
-        lsum += e;
-      }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    // O^T = V^T P^T, the P tile split per 32-key step straight from the score registers
-    f32x4 acc[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int v = 0; v < 4; ++v) acc[j][v] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKT / 2; ++ks) {
-      bf16x8 ph, pl;
-      split8(sc[2 * ks], sc[2 * ks + 1], ph, pl);
+      bf16x8 ph[NB], pl[NB];
 #pragma unroll
-      for (int v = 0; v < 4; ++v)
-        acc[v] = mfma3(frag_tr(Vh, ks * 32, v * 16, lane), frag_tr(Vl, ks * 32, v * 16, lane), ph, pl, acc[v]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (q < N) {
-      const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-      float* orow = p.o + ((int64_t)b * N + q) * D + h * 64;
+      for (int j = 0; j < NB; ++j) split8(sc[j][2 * ks], sc[j][2 * ks + 1], ph[j], pl[j]);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float w[4] = {acc[v][0] * inv, acc[v][1] * inv, acc[v][2] * inv, acc[v][3] * inv};
-        store4(orow + v * 16 + 4 * g, w);
+        const bf16x8 fh = frag_tr(Vh, ks * 32, v * 16, lane), fl = frag_tr(Vl, ks * 32, v * 16, lane);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j][v] = mfma3(fh, fl, ph[j], pl[j], acc[j][v]);
       }
-      if (g == 0) p.lse[((int64_t)b * p.H + h) * N + q] = lsum > 0.f ? (mref + __log2f(lsum)) * LN2 : NEG_INF;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (q[j] < N) {
+        const float inv = lsum[j] > 0.f ? 1.f / lsum[j] : 0.f;
+        float* orow = p.o + ((int64_t)b * N + q[j]) * D + h * 64;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float w[4] = {acc[j][v][0] * inv, acc[j][v][1] * inv, acc[j][v][2] * inv, acc[j][v][3] * inv};
+          store4(orow + v * 16 + 4 * g, w);
+        }
+        if (g == 0)
+          p.lse[((int64_t)b * p.H + h) * N + q[j]] = lsum[j] > 0.f ? (mref[j] + __log2f(lsum[j])) * LN2 : NEG_INF;
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------ backward
-template <bool CAUSAL>
+// NBA / NBB: key blocks per wave in phase A, query blocks per wave in phase B (2: every fragment read from the
+// images serves two blocks' products; 1: the one-block form, A/B)
+template <bool CAUSAL, int NBA, int NBB>
 __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
@@ -233,57 +259,87 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
   const int g = lane >> 4, li = lane & 15;
   const int nkb = NPAD >> 4, nstep = NPAD >> 5;
 
-  // ---- phase A: dK, dV for 16 keys per wave (Q images i0, dO images i1)
-  for (int kb = wave; kb < nkb; kb += 8) {
-    const int key = kb * 16 + li;
-    const bool kok = keyok[key];
-    bf16x8 kh[2], kl[2], vh[2], vl[2];
+  // ---- phase A: dK, dV for NB blocks of 16 keys per wave at a time (Q images i0, dO images i1): every Q / dO
+  // fragment read serves the NB blocks' products
+  for (int kb0 = wave * NBA; kb0 < nkb; kb0 += 8 * NBA) {
+    int key[NBA];
+    bool kok[NBA];
+    bf16x8 kh[NBA][2], kl[NBA][2], vh[NBA][2], vl[NBA][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      gfrag_x3(base + D, ld, key, N, kk, g, kh[kk], kl[kk]);
-      gfrag_x3(base + 2 * D, ld, key, N, kk, g, vh[kk], vl[kk]);
+    for (int j = 0; j < NBA; ++j) {
+      key[j] = (kb0 + j) * 16 + li;  // a block past nkb (NPAD >= its rows) computes P = 0 and stores nothing
+      kok[j] = key[j] < NPAD && keyok[key[j]];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        gfrag_x3(base + D, ld, key[j], N, kk, g, kh[j][kk], kl[j][kk]);
+        gfrag_x3(base + 2 * D, ld, key[j], N, kk, g, vh[j][kk], vl[j][kk]);
+      }
     }
-    f32x4 dv[4], dk[4];
+    f32x4 dv[NBA][4], dk[NBA][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) { dv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[u] = dv[u]; }
+    for (int j = 0; j < NBA; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { dv[j][u] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[j][u] = dv[j][u]; }
     for (int qs = 0; qs < nstep; ++qs) {
-      if (CAUSAL && qs * 32 + 31 < kb * 16) continue;  // every query of this step precedes every key
-      f32x4 pt[2], ds[2];
+      if (CAUSAL && qs * 32 + 31 < kb0 * 16) continue;  // every query of this step precedes every key
+      f32x4 pt[NBA][2], ds[NBA][2];
 #pragma unroll
       for (int tau = 0; tau < 2; ++tau) {
-        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+        f32x4 sc[NBA], dp[NBA];
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) { sc[j] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[j] = sc[j]; }
         const int qr = qs * 32 + tau * 16 + li;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          sc = mfma3(frag_row(i0h, qr, kk * 4 + g), frag_row(i0l, qr, kk * 4 + g), kh[kk], kl[kk], sc);
-          dp = mfma3(frag_row(i1h, qr, kk * 4 + g), frag_row(i1l, qr, kk * 4 + g), vh[kk], vl[kk], dp);
+          const bf16x8 qfh = frag_row(i0h, qr, kk * 4 + g), qfl = frag_row(i0l, qr, kk * 4 + g);
+          const bf16x8 ofh = frag_row(i1h, qr, kk * 4 + g), ofl = frag_row(i1l, qr, kk * 4 + g);
+#pragma unroll
+          for (int j = 0; j < NBA; ++j) {
+            sc[j] = mfma3(qfh, qfl, kh[j][kk], kl[j][kk], sc[j]);
+            dp[j] = mfma3(ofh, ofl, vh[j][kk], vl[j][kk], dp[j]);
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = qs * 32 + tau * 16 + 4 * g + r;
-          const bool ok = kok && (!CAUSAL || key <= q);
-          const float pv = ok ? exp2f(sc[r] * c2 - lse2[q]) : 0.f;
-          pt[tau][r] = pv;
-          ds[tau][r] = pv * (dp[r] - delta[q]);
+          const float l2 = lse2[q], dl = delta[q];
+#pragma unroll
+          for (int j = 0; j < NBA; ++j) {
+            const bool ok = kok[j] && (!CAUSAL || key[j] <= q);
+            const float pv = ok ? exp2f(sc[j][r] * c2 - l2) : 0.f;
+            pt[j][tau][r] = pv;
+            ds[j][tau][r] = pv * (dp[j][r] - dl);
+          }
         }
       }
-      bf16x8 ph, pl, sh, sl;
-      split8(pt[0], pt[1], ph, pl);
-      split8(ds[0], ds[1], sh, sl);
+      bf16x8 ph[NBA], pl[NBA], sh[NBA], sl[NBA];
+#pragma unroll
+      for (int j = 0; j < NBA; ++j) {
+        split8(pt[j][0], pt[j][1], ph[j], pl[j]);
+        split8(ds[j][0], ds[j][1], sh[j], sl[j]);
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        dv[u] = mfma3(frag_tr(i1h, qs * 32, u * 16, lane), frag_tr(i1l, qs * 32, u * 16, lane), ph, pl, dv[u]);
-        dk[u] = mfma3(frag_tr(i0h, qs * 32, u * 16, lane), frag_tr(i0l, qs * 32, u * 16, lane), sh, sl, dk[u]);
+        const bf16x8 ofh = frag_tr(i1h, qs * 32, u * 16, lane), ofl = frag_tr(i1l, qs * 32, u * 16, lane);
+        const bf16x8 qfh = frag_tr(i0h, qs * 32, u * 16, lane), qfl = frag_tr(i0l, qs * 32, u * 16, lane);
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) {
+          dv[j][u] = mfma3(ofh, ofl, ph[j], pl[j], dv[j][u]);
+          dk[j][u] = mfma3(qfh, qfl, sh[j], sl[j], dk[j][u]);
+        }
       }
     }
-    if (key < N) {
-      float* row = p.dqkv + ((int64_t)b * N + key) * ld + h * 64;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float a[4] = {dk[u][0] * p.scale, dk[u][1] * p.scale, dk[u][2] * p.scale, dk[u][3] * p.scale};
-        float c[4] = {dv[u][0], dv[u][1], dv[u][2], dv[u][3]};
-        store4(row + D + u * 16 + 4 * g, a);
-        store4(row + 2 * D + u * 16 + 4 * g, c);
+    for (int j = 0; j < NBA; ++j) {
+      if (key[j] < N) {
+        float* row = p.dqkv + ((int64_t)b * N + key[j]) * ld + h * 64;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float a[4] = {dk[j][u][0] * p.scale, dk[j][u][1] * p.scale, dk[j][u][2] * p.scale, dk[j][u][3] * p.scale};
+          float c[4] = {dv[j][u][0], dv[j][u][1], dv[j][u][2], dv[j][u][3]};
+          store4(row + D + u * 16 + 4 * g, a);
+          store4(row + 2 * D + u * 16 + 4 * g, c);
+        }
       }
     }
   }
@@ -292,63 +348,107 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
   stage_x3(i1h, i1l, base + 2 * D, ld, N, NPAD, t, 512);
   __syncthreads();
 
-  // ---- phase B: dQ for 16 queries per wave (K images i0, V images i1)
+  // ---- phase B: dQ for NB blocks of 16 queries per wave at a time (K images i0, V images i1)
   const int nqb = (N + 15) >> 4;
-  for (int qb = wave; qb < nqb; qb += 8) {
-    const int q = qb * 16 + li;
-    const float l2 = lse2[q], dl = delta[q];
-    bf16x8 qh[2], ql[2], oh[2], ol[2];
+  for (int qb0 = wave * NBB; qb0 < nqb; qb0 += 8 * NBB) {
+    int q[NBB];
+    float l2[NBB], dl[NBB];
+    bf16x8 qh[NBB][2], ql[NBB][2], oh[NBB][2], ol[NBB][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      gfrag_x3(base, ld, q, N, kk, g, qh[kk], ql[kk]);
-      gfrag_x3(dob, D, q, N, kk, g, oh[kk], ol[kk]);
+    for (int j = 0; j < NBB; ++j) {
+      q[j] = (qb0 + j) * 16 + li;  // a block past nqb computes on zero rows and stores nothing
+      l2[j] = q[j] < NPAD ? lse2[q[j]] : __builtin_huge_valf();
+      dl[j] = q[j] < NPAD ? delta[q[j]] : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        gfrag_x3(base, ld, q[j], N, kk, g, qh[j][kk], ql[j][kk]);
+        gfrag_x3(dob, D, q[j], N, kk, g, oh[j][kk], ol[j][kk]);
+      }
     }
-    f32x4 dq[4];
+    f32x4 dq[NBB][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dq[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NBB; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dq[j][u] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < nstep; ++ks) {
-      if (CAUSAL && ks * 32 > qb * 16 + 15) break;
-      f32x4 ds[2];
+      if (CAUSAL && ks * 32 > (qb0 + NBB - 1) * 16 + 15) break;
+      f32x4 ds[NBB][2];
 #pragma unroll
       for (int tau = 0; tau < 2; ++tau) {
-        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sc;
+        f32x4 sc[NBB], dp[NBB];
+#pragma unroll
+        for (int j = 0; j < NBB; ++j) { sc[j] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[j] = sc[j]; }
         const int kr = ks * 32 + tau * 16 + li;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          sc = mfma3(frag_row(i0h, kr, kk * 4 + g), frag_row(i0l, kr, kk * 4 + g), qh[kk], ql[kk], sc);
-          dp = mfma3(frag_row(i1h, kr, kk * 4 + g), frag_row(i1l, kr, kk * 4 + g), oh[kk], ol[kk], dp);
+          const bf16x8 kfh = frag_row(i0h, kr, kk * 4 + g), kfl = frag_row(i0l, kr, kk * 4 + g);
+          const bf16x8 vfh = frag_row(i1h, kr, kk * 4 + g), vfl = frag_row(i1l, kr, kk * 4 + g);
+#pragma unroll
+          for (int j = 0; j < NBB; ++j) {
+            sc[j] = mfma3(kfh, kfl, qh[j][kk], ql[j][kk], sc[j]);
+            dp[j] = mfma3(vfh, vfl, oh[j][kk], ol[j][kk], dp[j]);
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = ks * 32 + tau * 16 + 4 * g + r;
-          const bool ok = keyok[key] && (!CAUSAL || key <= q);
-          const float pv = ok ? exp2f(sc[r] * c2 - l2) : 0.f;
-          ds[tau][r] = pv * (dp[r] - dl);
+          const bool kok = keyok[key];
+#pragma unroll
+          for (int j = 0; j < NBB; ++j) {
+            const bool ok = kok && (!CAUSAL || key <= q[j]);
+            const float pv = ok ? exp2f(sc[j][r] * c2 - l2[j]) : 0.f;
+            ds[j][tau][r] = pv * (dp[j][r] - dl[j]);
+          }
         }
       }
-      bf16x8 sh, sl;
-      split8(ds[0], ds[1], sh, sl);
+      bf16x8 sh[NBB], sl[NBB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        dq[u] = mfma3(frag_tr(i0h, ks * 32, u * 16, lane), frag_tr(i0l, ks * 32, u * 16, lane), sh, sl, dq[u]);
-    }
-    if (q < N) {
-      float* row = p.dqkv + ((int64_t)b * N + q) * ld + h * 64;
+      for (int j = 0; j < NBB; ++j) split8(ds[j][0], ds[j][1], sh[j], sl[j]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float a[4] = {dq[u][0] * p.scale, dq[u][1] * p.scale, dq[u][2] * p.scale, dq[u][3] * p.scale};
-        store4(row + u * 16 + 4 * g, a);
+        const bf16x8 kfh = frag_tr(i0h, ks * 32, u * 16, lane), kfl = frag_tr(i0l, ks * 32, u * 16, lane);
+#pragma unroll
+        for (int j = 0; j < NBB; ++j) dq[j][u] = mfma3(kfh, kfl, sh[j], sl[j], dq[j][u]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NBB; ++j) {
+      if (q[j] < N) {
+        float* row = p.dqkv + ((int64_t)b * N + q[j]) * ld + h * 64;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float a[4] = {dq[j][u][0] * p.scale, dq[j][u][1] * p.scale, dq[j][u][2] * p.scale, dq[j][u][3] * p.scale};
+          store4(row + u * 16 + 4 * g, a);
+        }
       }
     }
   }
+}
+
+// blocks per wave (tools/attn_x3_bench.py, profiles/r06_attn_x3_blocks_ab.log): the unmasked forward takes two
+// (ViT-B/16 890 -> 845 us), the masked forward and the backward one (text forward 140 vs 173 us; backward equal
+// within 1 %, two key blocks spill); CLIPMI_ATTN_X3_NB=1 / 2 forces either (A/B, read per call)
+int x3_nb(bool fwd_unmasked) {
+  const char* e = getenv("CLIPMI_ATTN_X3_NB");
+  if (e && (atoi(e) == 1 || atoi(e) == 2)) return atoi(e);
+  return fwd_unmasked ? 2 : 1;
 }
 
 template <int NKT, bool M>
 void launch_fwd_x3(const AttnX& p, int causal, hipStream_t s) {
   constexpr size_t lds = 4 * (size_t)NKT * 16 * 128 + (size_t)NKT * 16 * sizeof(int);
   static_assert(lds <= 160 * 1024, "attn_fwd_x3: LDS");
-  (void)lds_optin((const void*)attn_fwd_x3<NKT, M>, (int)lds);
-  hipLaunchKernelGGL((attn_fwd_x3<NKT, M>), dim3(p.B * p.H), dim3(512), lds, s, p, causal);
+  // two blocks per wave spill (25-65 VGPRs) only in the masked forms from NKT = 14 on, which keep one
+  constexpr bool TWO = !(M && NKT >= 14);
+  if constexpr (TWO) {
+    if (x3_nb(!M) == 2) {
+      (void)lds_optin((const void*)attn_fwd_x3<NKT, M, 2>, (int)lds);
+      hipLaunchKernelGGL((attn_fwd_x3<NKT, M, 2>), dim3(p.B * p.H), dim3(512), lds, s, p, causal);
+      return;
+    }
+  }
+  (void)lds_optin((const void*)attn_fwd_x3<NKT, M, 1>, (int)lds);
+  hipLaunchKernelGGL((attn_fwd_x3<NKT, M, 1>), dim3(p.B * p.H), dim3(512), lds, s, p, causal);
 }
 
 template <bool M>
@@ -365,6 +465,18 @@ int fwd_x3_dispatch(const AttnX& p, int causal, hipStream_t s) {
     case 18: launch_fwd_x3<18, M>(p, causal, s); return CLIPMI_OK;
     default: return clipmi_invalid("attention_x3: N must be <= 288");
   }
+}
+
+// phase A's key blocks per wave with CLIPMI_ATTN_X3_NB=2: CLIPMI_ATTN_X3_NBA (default 1: two blocks spill 6-14
+// VGPRs there)
+int x3_nba() {
+  const char* e = getenv("CLIPMI_ATTN_X3_NBA");
+  return (e && atoi(e) == 2) ? 2 : 1;
+}
+template <bool C, int NBA, int NBB>
+void launch_bwd_x3(const AttnX& p, size_t lds, hipStream_t s) {
+  (void)lds_optin((const void*)attn_bwd_x3<C, NBA, NBB>, (int)lds);
+  hipLaunchKernelGGL((attn_bwd_x3<C, NBA, NBB>), dim3(p.B * p.H), dim3(512), lds, s, p);
 }
 
 size_t bwd_x3_lds(int N) {
@@ -419,12 +531,16 @@ extern "C" int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 10.0 * B * H * (double)N * npad * 64;
   ProfScope ps(s, "attn_bwd_x3", flops);
-  if (causal) {
-    (void)lds_optin((const void*)attn_bwd_x3<true>, (int)lds);
-    hipLaunchKernelGGL(attn_bwd_x3<true>, dim3(B * H), dim3(512), lds, s, p);
+  const int nb = x3_nb(false), nba = x3_nba();
+  if (nb == 1) {
+    if (causal) launch_bwd_x3<true, 1, 1>(p, lds, s);
+    else launch_bwd_x3<false, 1, 1>(p, lds, s);
+  } else if (nba == 2) {
+    if (causal) launch_bwd_x3<true, 2, 2>(p, lds, s);
+    else launch_bwd_x3<false, 2, 2>(p, lds, s);
   } else {
-    (void)lds_optin((const void*)attn_bwd_x3<false>, (int)lds);
-    hipLaunchKernelGGL(attn_bwd_x3<false>, dim3(B * H), dim3(512), lds, s, p);
+    if (causal) launch_bwd_x3<true, 1, 2>(p, lds, s);
+    else launch_bwd_x3<false, 1, 2>(p, lds, s);
   }
   ps.finish("attn_bwd_x3", flops);
   CLIPMI_CHECK_LAUNCH();
