@@ -263,6 +263,13 @@ int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, float* lse, 
                             int causal, int B, int H, int N, int D);
 int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void* o, const float* lse, const void* dout,
                             void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
+/* clipmi_attention_bwd_x3 with d_qkv written as its pattern-1 split image dimg bf16 [B*N][9D] (the layout of
+   clipmi_split3_colsum) and d_qkv's column sums (the q / k / v bias gradient) added onto colsum[3D] (+= when beta),
+   instead of the fp32 dqkv; N <= 288, ws >= clipmi_attention_bwd_x3img_ws(B, D) bytes, 256-byte aligned. */
+int64_t clipmi_attention_bwd_x3img_ws(int B, int D);
+int clipmi_attention_bwd_x3img(void* stream, const void* qkv, const void* o, const float* lse, const void* dout,
+                               void* dimg, float* colsum, int beta, void* ws, int64_t ws_bytes,
+                               const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 
 /* ---- Encoder engine: whole CLIPEncoder fwd/bwd in one call ([HF] :477-482, :362-383) ---------- */
 typedef struct clipmi_layer_w { /* activation dtype; qkv_w = [q;k;v] rows, [3D, D] */

@@ -173,6 +173,41 @@ def test_attention_x3(B, N, H, causal):
     assert max(e_g) < 3e-4, e_g
 
 
+@pytest.mark.parametrize("B,N,H,causal", [(3, 17, 2, False), (2, 197, 12, False), (5, 77, 8, True),
+                                           (3, 288, 2, False), (40, 197, 12, False)])
+def test_attention_bwd_x3img_matches_fp32_then_split(B, N, H, causal):
+    """clipmi_attention_bwd_x3img (the bf16x3 engine's attention backward since round 6): d_qkv written as its
+    pattern-1 split image and its column sums (the qkv bias gradient) added onto colsum -- bit for bit the image
+    clipmi_split3_colsum makes of clipmi_attention_bwd_x3's fp32 d_qkv, the sums against fp64."""
+    D = H * 64
+    qkv = rnd((B * N, 3 * D), 41, torch.float32)
+    mask = None
+    if causal:
+        g = torch.Generator().manual_seed(42)
+        lens = torch.randint(5, N + 1, (B,), generator=g)
+        mask = (torch.arange(N)[None] < lens[:, None]).to(torch.int64).cuda()
+    mp = mask.data_ptr() if mask is not None else None
+    o = torch.empty(B * N, D, device="cuda")
+    lse = torch.empty(B * H * N, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_attention_fwd_x3", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), mp, int(causal), B, H, N, D)
+    do = rnd((B * N, D), 43, torch.float32)
+    dqkv = torch.empty_like(qkv)
+    T.call("clipmi_attention_bwd_x3", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+           dqkv.data_ptr(), mp, int(causal), B, H, N, D)
+    img = torch.full((B * N, 9 * D), float("nan"), dtype=torch.bfloat16, device="cuda")
+    cs0 = rnd((3 * D,), 44, torch.float32)
+    cs = cs0.clone()
+    ws = T._ws(T._lib.lib().clipmi_attention_bwd_x3img_ws(B, D), "cuda")
+    T.call("clipmi_attention_bwd_x3img", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+           img.data_ptr(), cs.data_ptr(), 1, ws.data_ptr(), ws.numel(), mp, int(causal), B, H, N, D)
+    assert torch.equal(img, _split_ref(dqkv, 1))
+    assert rel(cs - cs0, dqkv.double().sum(0)) < 1e-5
+    with pytest.raises(ValueError, match="N <= 288"):
+        T.call("clipmi_attention_bwd_x3img", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
+               img.data_ptr(), cs.data_ptr(), 1, ws.data_ptr(), ws.numel(), mp, int(causal), 1, H, 300, D)
+
+
 def attn_ref64(qkv, B, N, H, mask, causal):
     D = H * 64
     q, k, v = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)

@@ -35,7 +35,37 @@ struct AttnX {
   const float* dout; float* dqkv;
   int B, H, N, D;
   float scale;
+  // image output of the backward (clipmi_attention_bwd_x3img): d_qkv as its pattern-1 split image [B*N][9D] and the
+  // per-batch-row column sums of d_qkv colp[B][3D] (the qkv bias gradient's partials)
+  bf16* dimg; float* colp;
 };
+
+// four fp32 values of an output row -> the pattern-1 image segments (h, l, h) at row + c, + seg, + 2 seg, with the
+// rounding of clipmi_split3_colsum (no contraction of v - h into a producing multiply)
+__device__ __forceinline__ void st_x3_4(bf16* row, int64_t seg, int c, const float v[4]) {
+#pragma clang fp contract(off)
+  bf16x4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (bf16)v[j];
+    l[j] = (bf16)(v[j] - (float)h[j]);
+  }
+  *(bf16x4*)(row + c) = h;
+  *(bf16x4*)(row + seg + c) = l;
+  *(bf16x4*)(row + 2 * seg + c) = h;
+}
+
+// sum of v over the 16 row lanes (li) of each lane group g, added by lane li == 0 into red[c .. c + 3]
+__device__ __forceinline__ void colsum16_add(float* red, int c, float v[4], int li) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v[r] += __shfl_xor(v[r], o, 64);
+  if (li == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[c + r] += v[r];
+  }
+}
 
 // 8 fp32 values -> hi / lo bf16 fragments
 __device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, bf16x8& h, bf16x8& l) {
@@ -208,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_x3(AttnX p, int causal) {
 // ------------------------------------------------------------------------------------------ backward
 // NBA / NBB: key blocks per wave in phase A, query blocks per wave in phase B (2: every fragment read from the
 // images serves two blocks' products; 1: the one-block form, A/B)
-template <bool CAUSAL, int NBA, int NBB>
+template <bool CAUSAL, int NBA, int NBB, bool XIMG = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
@@ -225,8 +255,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
   float* lse2 = (float*)(smem + 4 * IMG);
   float* delta = lse2 + NPAD;
   int* keyok = (int*)(delta + NPAD);
+  float* red = (float*)(keyok + NPAD);  // XIMG: per-wave column sums [8 waves][q, k, v][64]
   const float* base = p.qkv + (int64_t)b * N * ld + h * 64;
   const float* dob = p.dout + (int64_t)b * N * D + h * 64;
+  if (XIMG)
+    for (int i = t; i < 8 * 192; i += 512) red[i] = 0.f;
   stage_x3(i0h, i0l, base, ld, N, NPAD, t, 512);
   stage_x3(i1h, i1l, dob, D, N, NPAD, t, 512);
   {  // delta[q] = sum_d dO * O in fp32, 8 lanes per row
@@ -331,7 +364,20 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
     }
 #pragma unroll
     for (int j = 0; j < NBA; ++j) {
-      if (key[j] < N) {
+      if (XIMG) {  // rows past N hold exact zeros (P = dS = 0 there): summed as they are
+        bf16* row = p.dimg + ((int64_t)b * N + key[j]) * 3 * ld + h * 64;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float a[4] = {dk[j][u][0] * p.scale, dk[j][u][1] * p.scale, dk[j][u][2] * p.scale, dk[j][u][3] * p.scale};
+          float c[4] = {dv[j][u][0], dv[j][u][1], dv[j][u][2], dv[j][u][3]};
+          if (key[j] < N) {
+            st_x3_4(row, ld, D + u * 16 + 4 * g, a);
+            st_x3_4(row, ld, 2 * D + u * 16 + 4 * g, c);
+          }
+          colsum16_add(red + wave * 192 + 64, u * 16 + 4 * g, a, li);
+          colsum16_add(red + wave * 192 + 128, u * 16 + 4 * g, c, li);
+        }
+      } else if (key[j] < N) {
         float* row = p.dqkv + ((int64_t)b * N + key[j]) * ld + h * 64;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -413,7 +459,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
     }
 #pragma unroll
     for (int j = 0; j < NBB; ++j) {
-      if (q[j] < N) {
+      if (XIMG) {  // rows past N: zero query rows give dS = 0 (dO = 0 there), dq = 0
+        bf16* row = p.dimg + ((int64_t)b * N + q[j]) * 3 * ld + h * 64;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float a[4] = {dq[j][u][0] * p.scale, dq[j][u][1] * p.scale, dq[j][u][2] * p.scale, dq[j][u][3] * p.scale};
+          if (q[j] < N) st_x3_4(row, ld, u * 16 + 4 * g, a);
+          if (q[j] >= N) a[0] = a[1] = a[2] = a[3] = 0.f;
+          colsum16_add(red + wave * 192, u * 16 + 4 * g, a, li);
+        }
+      } else if (q[j] < N) {
         float* row = p.dqkv + ((int64_t)b * N + q[j]) * ld + h * 64;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -421,6 +476,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_x3(AttnX p) {
           store4(row + u * 16 + 4 * g, a);
         }
       }
+    }
+  }
+  if (XIMG) {  // the workgroup's column sums in wave order -> colp[b][q | k | v columns of head h]
+    __syncthreads();
+    if (t < 192) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += red[w * 192 + t];
+      p.colp[(int64_t)b * 3 * D + (t >> 6) * D + h * 64 + (t & 63)] = sum;
     }
   }
 }
@@ -473,15 +537,15 @@ int x3_nba() {
   const char* e = getenv("CLIPMI_ATTN_X3_NBA");
   return (e && atoi(e) == 2) ? 2 : 1;
 }
-template <bool C, int NBA, int NBB>
+template <bool C, int NBA, int NBB, bool IMG = false>
 void launch_bwd_x3(const AttnX& p, size_t lds, hipStream_t s) {
-  (void)lds_optin((const void*)attn_bwd_x3<C, NBA, NBB>, (int)lds);
-  hipLaunchKernelGGL((attn_bwd_x3<C, NBA, NBB>), dim3(p.B * p.H), dim3(512), lds, s, p);
+  (void)lds_optin((const void*)attn_bwd_x3<C, NBA, NBB, IMG>, (int)lds);
+  hipLaunchKernelGGL((attn_bwd_x3<C, NBA, NBB, IMG>), dim3(p.B * p.H), dim3(512), lds, s, p);
 }
 
 size_t bwd_x3_lds(int N) {
   const size_t npad = (size_t)((N + 31) & ~31);
-  return 4 * npad * 128 + 3 * npad * 4;
+  return 4 * npad * 128 + 3 * npad * 4 + 8 * 192 * 4;  // images, lse2 / delta / keyok, the image form's column sums
 }
 
 }  // namespace
@@ -501,7 +565,7 @@ extern "C" int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, f
   if (N > X3_MAX_N) return clipmi_attention_fwd(stream, CLIPMI_F32, qkv, o, lse, attention_mask, causal, B, H, N, D);
   if (B == 0) return CLIPMI_OK;
   CLIPMI_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)o & 15) == 0, "qkv / o must be 16-byte aligned");
-  AttnX p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f};
+  AttnX p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f, nullptr, nullptr};
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 4.0 * B * H * (double)N * npad * 64;  // the MFMA work issued: three products each
   ProfScope ps(s, "attn_fwd_x3", flops);
@@ -526,7 +590,7 @@ extern "C" int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void
                      ((uintptr_t)dqkv & 15) == 0,
                  "qkv / o / dout / dqkv must be 16-byte aligned");
   AttnX p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D,
-          0.125f};
+          0.125f, nullptr, nullptr};
   const size_t lds = bwd_x3_lds(N);
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 10.0 * B * H * (double)N * npad * 64;
@@ -543,6 +607,44 @@ extern "C" int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void
     else launch_bwd_x3<false, 1, 2>(p, lds, s);
   }
   ps.finish("attn_bwd_x3", flops);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// The same backward with d_qkv written as its pattern-1 split image dimg bf16 [B*N][9D] (segments h, l, h at columns
+// c, 3D + c, 6D + c: clipmi_split3_colsum's layout and rounding) and its column sums -- the q / k / v bias gradient --
+// added onto colsum[3D] (+= when beta): the bf16x3 engine's input to the qkv weight and input gradients, without an
+// fp32 d_qkv and a split pass over it.  N <= 288; ws >= clipmi_attention_bwd_x3img_ws(B, D) bytes, 256-B aligned.
+extern "C" int64_t clipmi_attention_bwd_x3img_ws(int B, int D) {
+  return B > 0 && D > 0 ? colsum_partials_ws(B, 3 * D) : 0;
+}
+extern "C" int clipmi_attention_bwd_x3img(void* stream, const void* qkv, const void* o, const float* lse,
+                                          const void* dout, void* dimg, float* colsum, int beta, void* ws,
+                                          int64_t ws_bytes, const int64_t* attention_mask, int causal, int B, int H,
+                                          int N, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
+  CLIPMI_REQUIRE(N >= 1 && N <= X3_MAX_N, "attention_bwd_x3img: 1 <= N <= 288");
+  CLIPMI_REQUIRE(qkv && o && lse && dout && dimg && colsum, "operands");
+  CLIPMI_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)o & 15) == 0 && ((uintptr_t)dout & 15) == 0 &&
+                     ((uintptr_t)dimg & 7) == 0,
+                 "qkv / o / dout 16-byte, dimg 8-byte aligned");
+  CLIPMI_REQUIRE(ws && ws_bytes >= clipmi_attention_bwd_x3img_ws(B, D) && ((uintptr_t)ws & 255) == 0,
+                 "attention_bwd_x3img: workspace (clipmi_attention_bwd_x3img_ws, 256-byte aligned)");
+  if (B == 0) return CLIPMI_OK;
+  float* colp = (float*)ws;
+  AttnX p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, nullptr, B, H, N, D, 0.125f,
+          (bf16*)dimg, colp};
+  const size_t lds = bwd_x3_lds(N);
+  const int npad = (N + 31) & ~31;
+  const double flops = 3 * 10.0 * B * H * (double)N * npad * 64;
+  ProfScope ps(s, "attn_bwd_x3", flops);
+  if (causal) launch_bwd_x3<true, 1, 1, true>(p, lds, s);
+  else launch_bwd_x3<false, 1, 1, true>(p, lds, s);
+  ps.finish("attn_bwd_x3", flops);
+  CLIPMI_CHECK_LAUNCH();
+  float* fold = (float*)((char*)ws + ((int64_t)B * 3 * D * 4 + 255) / 256 * 256);
+  CLIPMI_TRY(colsum_partials_finish(s, colp, B, 3 * D, colsum, beta, fold));
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }

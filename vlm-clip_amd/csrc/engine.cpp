@@ -151,8 +151,9 @@ X3Plan x3_plan(const clipmi_encoder_desc* d) {
     if (sp > 1) smax = std::max(smax, (int64_t)sp * w[0] * w[1] * 4);
   }
   p.col = p.slab + align256(smax);
-  p.total = p.col + align256(std::max(clipmi_split3_colsum_ws((int)R, (int)std::max(3 * D, F)),
-                                      clipmi_gemm_x3out_ws((int)R, (int)F)));
+  p.total = p.col + align256(std::max({clipmi_split3_colsum_ws((int)R, (int)std::max(3 * D, F)),
+                                       clipmi_gemm_x3out_ws((int)R, (int)F),
+                                       clipmi_attention_bwd_x3img_ws(d->B, (int)D)}));
   return p;
 }
 bool x3_mode(const clipmi_encoder_desc* d) { return d->gemm_x3 && d->dtype == CLIPMI_F32; }
@@ -386,9 +387,14 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
     CLIPMI_TRY(split_g(g2, D, g.out_b));                                                    // gbo += sum dh
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, D, gimg, w.out_w, dln, D, 0));                       // d_o = dh Wo
     CLIPMI_TRY(wgrad(D, D, gimg, x3_o3(a, R, D), g.out_w));                                 // gWo += dh^T o
-    CLIPMI_TRY(clipmi_attention_bwd_x3(s, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
-                                       d->N, D));                                           // d_qkv
-    CLIPMI_TRY(split_g(dbig, 3 * D, g.qkv_b));                                              // gbqkv += sum d_qkv
+    if (d->N <= 288) {  // d_qkv's image and gbqkv written by the attention backward itself
+      CLIPMI_TRY(clipmi_attention_bwd_x3img(s, a.qkv, a.o, a.lse, dln, gimg, g.qkv_b, 1, col, col_bytes,
+                                            d->attention_mask, d->causal, d->B, d->H, d->N, D));
+    } else {
+      CLIPMI_TRY(clipmi_attention_bwd_x3(s, a.qkv, a.o, a.lse, dln, dbig, d->attention_mask, d->causal, d->B, d->H,
+                                         d->N, D));                                         // d_qkv
+      CLIPMI_TRY(split_g(dbig, 3 * D, g.qkv_b));                                            // gbqkv += sum d_qkv
+    }
     CLIPMI_TRY(wgrad(3 * D, D, gimg, a.ln1, g.qkv_w));                                      // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, 3 * D, gimg, w.qkv_w, dln, D, 0));                   // d_ln1
     CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D,

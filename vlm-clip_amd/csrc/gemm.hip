@@ -1749,9 +1749,22 @@ constexpr int X3_FOLD = 64;  // first-stage groups of the column sums
 int x3out_parts(int M) { return (M + 127) / 128; }
 }  // namespace
 
+// colsum[N] (+= when beta) = sum of the P partial rows part[P][N]: groups of rows folded in order into fold[<= 64][N],
+// then those in order (norm.hip reduce_partials4_kernel); deterministic.  N % 4 == 0, 16-B aligned buffers.
+int colsum_partials_finish(hipStream_t s, const float* part, int P, int N, float* colsum, int beta, float* fold) {
+  const int per = (P + X3_FOLD - 1) / X3_FOLD, G = (P + per - 1) / per;
+  hipLaunchKernelGGL(fold_rows4_kernel, dim3((N / 4 + 255) / 256, G), dim3(256), 0, s, part, P, N, per, fold);
+  DeferredReduce r;
+  memset(&r, 0, sizeof(r));
+  r.kind = 2;
+  r.part = fold; r.stride = N; r.P = G; r.D = N; r.out = colsum; r.out2 = nullptr; r.pbeta = beta;
+  return launch_partials_reduce(s, r);
+}
+int64_t colsum_partials_ws(int P, int N) { return ((int64_t)P * N * 4 + 255) / 256 * 256 + (int64_t)X3_FOLD * N * 4; }
+
 extern "C" int64_t clipmi_gemm_x3out_ws(int M, int N) {
   if (M <= 0 || N <= 0) return 0;
-  return ((int64_t)x3out_parts(M) * N * 4 + 255) / 256 * 256 + (int64_t)X3_FOLD * N * 4;
+  return colsum_partials_ws(x3out_parts(M), N);
 }
 
 extern "C" int clipmi_gemm_x3out_ok(int M, int N, int K, int a_kmajor, int b_kmajor, int flags) {
@@ -1784,14 +1797,8 @@ extern "C" int clipmi_gemm_x3out(void* stream, const clipmi_gemm_desc* d, int pa
   CLIPMI_TRY(gemm_impl(stream, d, 1 + pattern, colp));
   if (colsum) {
     const int P = x3out_parts(d->M);
-    const int per = (P + X3_FOLD - 1) / X3_FOLD, G = (P + per - 1) / per;
     float* fold = (float*)((char*)ws + ((int64_t)P * d->N * 4 + 255) / 256 * 256);
-    hipLaunchKernelGGL(fold_rows4_kernel, dim3((d->N / 4 + 255) / 256, G), dim3(256), 0, s, colp, P, d->N, per, fold);
-    DeferredReduce r;
-    memset(&r, 0, sizeof(r));
-    r.kind = 2;
-    r.part = fold; r.stride = d->N; r.P = G; r.D = d->N; r.out = colsum; r.out2 = nullptr; r.pbeta = beta;
-    CLIPMI_TRY(launch_partials_reduce(s, r));
+    CLIPMI_TRY(colsum_partials_finish(s, colp, P, d->N, colsum, beta, fold));
   }
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;

@@ -68,3 +68,6 @@ DeferredReduce*& deferred_slot();
 // launch a recorded reduction on its own (the standalone kernels) and empty it
 int launch_deferred(hipStream_t s, DeferredReduce& r);
 int launch_partials_reduce(hipStream_t s, const DeferredReduce& r);  // kind 2 (norm.hip)
+// column sums from P partial rows [P][N] (+= when beta), deterministic; fold: 64 x N floats (gemm.hip)
+int colsum_partials_finish(hipStream_t s, const float* part, int P, int N, float* colsum, int beta, float* fold);
+int64_t colsum_partials_ws(int P, int N);  // bytes for the partial rows (256-B aligned) + fold
