@@ -251,6 +251,15 @@ int64_t clipmi_gemm_x3out_ws(int M, int N);
 int clipmi_gemm_x3out_ok(int M, int N, int K, int a_kmajor, int b_kmajor, int flags);
 int clipmi_gemm_x3out(void* stream, const clipmi_gemm_desc* d, int pattern, float* colsum, int beta, void* ws,
                       int64_t ws_bytes);
+/* bf16x3 engine: the fp32 LayerNorm backward (as clipmi_layernorm_bwd with dtype CLIPMI_F32, dw / db required) that
+   also writes dx as its pattern-1 split image dimg bf16 [R][3D] and adds dx's column sums onto colsum[D] (+= when
+   beta_cs) -- the next GEMMs' operand and a Linear's bias gradient without a split pass.  D / 64 in
+   {1, 2, 3, 4, 6, 8, 12, 16}; ws >= clipmi_layernorm_bwd_x3_ws(R, D) bytes, 16-byte aligned. */
+int64_t clipmi_layernorm_bwd_x3_ws(int R, int D);
+int clipmi_layernorm_bwd_x3(void* stream, const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* mean,
+                            const float* rstd, const float* w, float* dx, int64_t lddx, const float* dres,
+                            int64_t ldres, float* dw, float* db, int beta_wb, void* dimg, float* colsum, int beta_cs,
+                            void* ws, int64_t ws_bytes, int R, int D);
 /* LayerNorm of fp32 x with fp32 affine weights written as the bf16x3 split image y3 [R][3D] of its output
    (pattern as above); mean / rstd saved as in clipmi_layernorm_fwd.  D / 64 in {1, 2, 3, 4, 6, 8, 12, 16}. */
 int clipmi_layernorm_fwd_x3(void* stream, const float* x, int64_t ldx, void* y3, int pattern, const float* w,

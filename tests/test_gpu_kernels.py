@@ -766,6 +766,42 @@ def test_layernorm_bwd_any_width_lds_grows():
         assert rel(dx, xr.grad) < 1e-4 and rel(dw, wr.grad) < 1e-4 and rel(db, br.grad) < 1e-4, D
 
 
+@pytest.mark.parametrize("R,D", [(1000, 768), (77, 512), (5000, 768), (3, 1024)])
+def test_layernorm_bwd_x3_writes_dx_image_and_colsum(R, D):
+    """clipmi_layernorm_bwd_x3 (the bf16x3 engine's LayerNorm backwards since round 6): the fp32 backward with the
+    residual gradient, plus dx's pattern-1 split image (bit for bit clipmi_split3_colsum's image of the fp32 dx) and
+    dx's column sums added onto colsum (a Linear's bias gradient); dgamma / dbeta as the plain backward."""
+    x = rnd((R, D), 51, torch.float32)
+    w = rnd((D,), 52, torch.float32) * 0.2 + 1
+    b = rnd((D,), 53, torch.float32) * 0.1
+    dy = rnd((R, D), 54, torch.float32)
+    dres = rnd((R, D), 55, torch.float32)
+    y = torch.empty_like(x)
+    st = torch.empty(2, R, device="cuda")
+    s = kern.stream()
+    T.call("clipmi_layernorm_fwd", s, F32, x.data_ptr(), D, y.data_ptr(), D, w.data_ptr(), b.data_ptr(),
+           st[0].data_ptr(), st[1].data_ptr(), R, D, 1e-5, None, None, 0)
+    dx = torch.empty_like(x)
+    dw, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    ws = T._ws(T._lib.lib().clipmi_layernorm_bwd_ws(R, D), "cuda")
+    T.call("clipmi_layernorm_bwd", s, F32, dy.data_ptr(), D, x.data_ptr(), D, st[0].data_ptr(), st[1].data_ptr(),
+           w.data_ptr(), dx.data_ptr(), D, dres.data_ptr(), D, dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(),
+           ws.numel(), R, D)
+    dx3 = torch.empty_like(x)
+    dw3, db3 = torch.full((D,), 2.0, device="cuda"), torch.full((D,), 3.0, device="cuda")
+    img = torch.full((R, 3 * D), float("nan"), dtype=torch.bfloat16, device="cuda")
+    cs0 = rnd((D,), 56, torch.float32)
+    cs = cs0.clone()
+    ws3 = T._ws(T._lib.lib().clipmi_layernorm_bwd_x3_ws(R, D), "cuda")
+    T.call("clipmi_layernorm_bwd_x3", s, dy.data_ptr(), D, x.data_ptr(), D, st[0].data_ptr(), st[1].data_ptr(),
+           w.data_ptr(), dx3.data_ptr(), D, dres.data_ptr(), D, dw3.data_ptr(), db3.data_ptr(), 1, img.data_ptr(),
+           cs.data_ptr(), 1, ws3.data_ptr(), ws3.numel(), R, D)
+    assert torch.equal(dx3, dx)
+    assert torch.equal(img, _split_ref(dx, 1))
+    assert rel(dw3 - 2.0, dw) < 1e-6 and rel(db3 - 3.0, db) < 1e-6
+    assert rel(cs - cs0, dx.double().sum(0)) < 1e-5
+
+
 def _split_ref(x, pattern):
     """bf16x3 image of fp32 x [R, N]: [R, 3N] bf16, segments (h, h, l) (pattern 0) or (h, l, h) (pattern 1)."""
     h = x.to(torch.bfloat16)

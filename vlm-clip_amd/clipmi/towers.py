@@ -77,6 +77,9 @@ _lib.declare("clipmi_layernorm_bwd2", [c_vp, c_int, c_int, c_vp, c_i64, c_vp, c_
 _lib.declare("clipmi_layernorm_bwd3", [c_vp, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                        c_i64, c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
 _lib.declare("clipmi_layernorm_bwd_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_layernorm_bwd_x3_ws", [c_int, c_int], c_i64)
+_lib.declare("clipmi_layernorm_bwd_x3", [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
 _lib.declare("clipmi_layernorm_bwd", [c_vp, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
                                       c_i64, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int])
 _lib.declare("clipmi_colsum_ws", [c_int, c_int], c_i64)

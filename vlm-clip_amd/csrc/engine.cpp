@@ -233,7 +233,7 @@ WsPlan plan(const clipmi_encoder_desc* d) {
   if (d->dtype == CLIPMI_BF16) sp = 2 * align256(sp);
   p.colsum = p.split + align256(sp);
   p.ln = p.colsum + align256(clipmi_colsum_ws((int)R, (int)big));
-  p.total = p.ln + align256(clipmi_layernorm_bwd_ws((int)R, d->D));
+  p.total = p.ln + align256(std::max(clipmi_layernorm_bwd_ws((int)R, d->D), clipmi_layernorm_bwd_x3_ws((int)R, d->D)));
   return p;
 }
 
@@ -361,6 +361,11 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
   // fc2's input gradient writes d_pre's image itself where the fused form exists (dbig holds dx's image, 6 D B per
   // row, inside its 4 max(3D, F) B)
   const bool fuse_dpre = clipmi_gemm_x3out_ok(R, F, 3 * D, 1, 0, CLIPMI_EPI_MUL_AUX) && 3 * D <= 2 * std::max(3 * D, F);
+  // the LayerNorm backwards write their dx's image and its column sums too (clipmi_layernorm_bwd_x3): LN2's into gimg
+  // (dh, the out-projection's gradient) and LN1's into dbig (the next layer's dx) where fuse_dpre keeps it there
+  const bool ln_x3 = D % 64 == 0 && (D / 64 == 1 || D / 64 == 2 || D / 64 == 3 || D / 64 == 4 || D / 64 == 6 ||
+                                     D / 64 == 8 || D / 64 == 12 || D / 64 == 16);
+  bool dx_img = false;  // dbig holds dx's image and this layer's fc2 bias gradient already has its column sums
   for (int l = layer_hi - 1; l >= layer_lo; --l) {
     const clipmi_layer_w& w = d->layers[l];
     const clipmi_layer_act& a = d->act[l];
@@ -368,7 +373,8 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
     CLIPMI_REQUIRE(a.pre, "training forward must save pre-activations");
     // MLP branch: dx is dL/dy
     if (fuse_dpre) {  // d_pre's image written by fc2's input-gradient epilogue; dx's image in dbig meanwhile
-      CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)dx, D, R, D, dbig, 1, g.fc2_b, 1, col, col_bytes));  // gb2
+      if (!dx_img)
+        CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)dx, D, R, D, dbig, 1, g.fc2_b, 1, col, col_bytes));  // gb2
       CLIPMI_TRY(clipmi_split3(s, (const float*)w.fc2_w, F, F, D, 0, wimg, 0));
       CLIPMI_TRY(x3_gemm_img(s, R, F, 3 * D, dbig, 3 * (int64_t)D, wimg, (F + 7) / 8 * 8, false, gimg, 1,
                              CLIPMI_EPI_MUL_AUX, nullptr, a.pre, F, g.fc1_b, col, col_bytes));  // d_pre, gb1
@@ -381,10 +387,16 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
     }
     CLIPMI_TRY(wgrad(F, D, gimg, a.ln2, g.fc1_w));                                          // gW1 += d_pre^T ln2
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, F, gimg, w.fc1_w, dln, D, 0));                       // d_ln2 = d_pre W1
-    CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx,
-                                     D, g.ln2_w, g.ln2_b, 1, wln, ln_bytes, R, D));          // dh = dx + LN2'(d_ln2)
+    if (ln_x3) {  // dh = dx + LN2'(d_ln2), its image into gimg, gbo += sum dh
+      CLIPMI_TRY(clipmi_layernorm_bwd_x3(s, dln, D, (const float*)a.h, D, a.mean2, a.rstd2, (const float*)w.ln2_w, g2,
+                                         D, (const float*)dx, D, g.ln2_w, g.ln2_b, 1, gimg, g.out_b, 1, wln, ln_bytes,
+                                         R, D));
+    } else {
+      CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.h, D, a.mean2, a.rstd2, w.ln2_w, g2, D, dx,
+                                       D, g.ln2_w, g.ln2_b, 1, wln, ln_bytes, R, D));        // dh = dx + LN2'(d_ln2)
+      CLIPMI_TRY(split_g(g2, D, g.out_b));                                                  // gbo += sum dh
+    }
     // attention branch: g2 is dL/dh
-    CLIPMI_TRY(split_g(g2, D, g.out_b));                                                    // gbo += sum dh
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, D, gimg, w.out_w, dln, D, 0));                       // d_o = dh Wo
     CLIPMI_TRY(wgrad(D, D, gimg, x3_o3(a, R, D), g.out_w));                                 // gWo += dh^T o
     if (d->N <= 288) {  // d_qkv's image and gbqkv written by the attention backward itself
@@ -397,8 +409,15 @@ int encoder_bwd_x3(void* s, const clipmi_encoder_desc* d, void* dx, int layer_hi
     }
     CLIPMI_TRY(wgrad(3 * D, D, gimg, a.ln1, g.qkv_w));                                      // gWqkv += d_qkv^T ln1
     CLIPMI_TRY(x3_dgrad(s, wimg, R, D, 3 * D, gimg, w.qkv_w, dln, D, 0));                   // d_ln1
-    CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D,
-                                     g2, D, g.ln1_w, g.ln1_b, 1, wln, ln_bytes, R, D));     // dx_in = dh + LN1'(d_ln1)
+    dx_img = fuse_dpre && ln_x3 && l > layer_lo;
+    if (dx_img) {  // dx_in = dh + LN1'(d_ln1), its image into dbig, layer l - 1's gb2 += sum dx_in
+      CLIPMI_TRY(clipmi_layernorm_bwd_x3(s, dln, D, (const float*)a.x_in, D, a.mean1, a.rstd1, (const float*)w.ln1_w,
+                                         (float*)dx, D, g2, D, g.ln1_w, g.ln1_b, 1, dbig, d->grads[l - 1].fc2_b, 1,
+                                         wln, ln_bytes, R, D));
+    } else {
+      CLIPMI_TRY(clipmi_layernorm_bwd2(s, CLIPMI_F32, CLIPMI_F32, dln, D, a.x_in, D, a.mean1, a.rstd1, w.ln1_w, dx, D,
+                                       g2, D, g.ln1_w, g.ln1_b, 1, wln, ln_bytes, R, D));   // dx_in = dh + LN1'(d_ln1)
+    }
   }
   return CLIPMI_OK;
 }

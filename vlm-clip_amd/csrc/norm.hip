@@ -158,18 +158,38 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TX* x, int64_t ldx, T* y, i
 // per-block partial dgamma/dbeta -> ws[blockIdx][2][D]
 // TW: the affine weight's dtype (default T; fp32 for the vision pre_layrnorm, whose fp32-residual forward
 // normalises with the fp32 master weights)
-template <typename TX, typename T, int PS, int NP, typename TW = T>
+// PS fp32 values -> their split image segments at dst, dst + seg, dst + 2 seg ((h, h, l) for pattern 0, (h, l, h) for
+// 1) with clipmi_split3_colsum's rounding: l from the ROUNDED v (no contraction into a producing multiply)
+template <int PS>
+__device__ __forceinline__ void split_store_x3(bf16* dst, int64_t seg, const float* v, int pattern) {
+#pragma clang fp contract(off)
+  float hv[PS], lv[PS];
+#pragma unroll
+  for (int j = 0; j < PS; ++j) {
+    hv[j] = (float)(bf16)v[j];
+    lv[j] = v[j] - hv[j];
+  }
+  vstore<bf16, PS>(dst, hv);
+  vstore<bf16, PS>(dst + seg, pattern ? lv : hv);
+  vstore<bf16, PS>(dst + 2 * seg, pattern ? hv : lv);
+}
+
+// X3 (the bf16x3 engine, fp32 throughout): dx is also written as its pattern-1 split image img [R][3D] (segments
+// h, l, h; clipmi_split3_colsum's layout and rounding) and dx's column sums -- the bias gradient of the Linear whose
+// output gradient dx is -- join the partial rows: ws[blockIdx][3][D] (dgamma, dbeta, sum dx)
+template <typename TX, typename T, int PS, int NP, typename TW = T, bool X3 = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, const TX* x, int64_t ldx,
                                                      const float* mean, const float* rstd, const TW* w,
                                                      T* dx, int64_t lddx, const T* dres, int64_t ldres,
-                                                     float* ws, int R, int D) {
-  __shared__ float red[4][2][NP * PS * 64];
+                                                     float* ws, int R, int D, bf16* img) {
+  constexpr int NPR = X3 ? 3 : 2;
+  __shared__ float red[4][NPR][NP * PS * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pg[NP][PS], pb[NP][PS];
+  float pg[NP][PS], pb[NP][PS], pd[NP][PS];
 #pragma unroll
   for (int k = 0; k < NP; ++k)
 #pragma unroll
-    for (int j = 0; j < PS; ++j) { pg[k][j] = 0.f; pb[k][j] = 0.f; }
+    for (int j = 0; j < PS; ++j) { pg[k][j] = 0.f; pb[k][j] = 0.f; pd[k][j] = 0.f; }
   float wv[NP][PS];
 #pragma unroll
   for (int k = 0; k < NP; ++k) vload<TW, PS>(w + (k * 64 + lane) * PS, wv[k]);
@@ -228,6 +248,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
           if (dres) o[j] += rr[q][k][j];
         }
         vstore<T, PS>(dx + (int64_t)row * lddx + c, o);
+        if constexpr (X3) {
+          split_store_x3<PS>(img + (int64_t)row * 3 * D + c, D, o, 1);
+#pragma unroll
+          for (int j = 0; j < PS; ++j) pd[k][j] += o[j];
+        }
       }
     }
   }
@@ -238,13 +263,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* dy, int64_t lddy, 
     for (int j = 0; j < PS; ++j) {
       red[wave][0][(k * 64 + lane) * PS + j] = pg[k][j];
       red[wave][1][(k * 64 + lane) * PS + j] = pb[k][j];
+      if constexpr (X3) red[wave][2][(k * 64 + lane) * PS + j] = pd[k][j];
     }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += 256) {
-    float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    ws[(int64_t)blockIdx.x * 2 * D + c] = a;
-    ws[(int64_t)blockIdx.x * 2 * D + D + c] = bb;
+#pragma unroll
+    for (int u = 0; u < NPR; ++u)
+      ws[((int64_t)blockIdx.x * NPR + u) * D + c] = red[0][u][c] + red[1][u][c] + red[2][u][c] + red[3][u][c];
   }
 }
 
@@ -680,22 +705,30 @@ void ln_fwd_q8_launch(hipStream_t s, void* x, int64_t ldx, uint8_t* q8, uint8_t*
 // grid (in: the partial-sum rows the workspace holds; out: the blocks launched = partial rows
 // written): at most the blocks the CUs hold at once, so no block starts a second round late
 // (the D = 768 form keeps two rows' loads in registers: 164 VGPRs, 3 waves per SIMD)
-template <typename TX, typename T, int PS, int NP, typename TW = T>
+template <typename TX, typename T, int PS, int NP, typename TW = T, bool X3 = false>
 void ln_bwd_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
                    const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
-                   int64_t ldres, float* ws, int R, int D) {
+                   int64_t ldres, float* ws, int R, int D, void* img = nullptr) {
   static int resident = [] {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<TX, T, PS, NP, TW>, 256, 0) !=
-            hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<TX, T, PS, NP, TW, X3>, 256,
+                                                     0) != hipSuccess || per_cu < 1)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     return per_cu * cus;
   }();
   if (grid > resident) grid = resident;
-  hipLaunchKernelGGL((ln_bwd_kernel<TX, T, PS, NP, TW>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy, (const TX*)x,
-                     ldx, mean, rstd, (const TW*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D);
+  hipLaunchKernelGGL((ln_bwd_kernel<TX, T, PS, NP, TW, X3>), dim3(grid), dim3(256), 0, s, (const T*)dy, lddy,
+                     (const TX*)x, ldx, mean, rstd, (const TW*)w, (T*)dx, lddx, (const T*)dres, ldres, ws, R, D,
+                     (bf16*)img);
+}
+// the bf16x3 form (fp32 everything, dx's image + column sums)
+template <typename TX, typename T, int PS, int NP>
+void ln_bwd_x3_launch(hipStream_t s, int& grid, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                      const float* mean, const float* rstd, const void* w, void* dx, int64_t lddx, const void* dres,
+                      int64_t ldres, float* ws, int R, int D, void* img) {
+  ln_bwd_launch<TX, T, PS, NP, T, true>(s, grid, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, ws, R, D, img);
 }
 
 template <typename TX, typename T, int PS, int NP>
@@ -876,6 +909,39 @@ extern "C" int clipmi_layernorm_bwd3(void* stream, int x_dtype, int dtype, int w
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf, (int64_t)2 * D, nb, D, dw, (float*)nullptr, beta_wb);
   else if (db)
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((D + 63) / 64), dim3(1024), 0, s, wsf + D, (int64_t)2 * D, nb, D, db, (float*)nullptr, beta_wb);
+  CLIPMI_CHECK_LAUNCH();
+  return CLIPMI_OK;
+}
+
+// bf16x3 engine: clipmi_layernorm_bwd (fp32 throughout, D / 64 in {1, 2, 3, 4, 6, 8, 12, 16}) that also writes dx as
+// its pattern-1 split image dimg [R][3D] and adds dx's column sums onto colsum[D] (+= when beta_cs): the next
+// GEMMs' operand and the bias gradient of the Linear whose output gradient dx is, without a split pass.  dw / db are
+// required; ws >= clipmi_layernorm_bwd_x3_ws(R, D) bytes, 16-byte aligned.
+extern "C" int64_t clipmi_layernorm_bwd_x3_ws(int R, int D) { return clipmi_layernorm_bwd_ws(R, D) / 2 * 3; }
+extern "C" int clipmi_layernorm_bwd_x3(void* stream, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                                       const float* mean, const float* rstd, const float* w, float* dx, int64_t lddx,
+                                       const float* dres, int64_t ldres, float* dw, float* db, int beta_wb, void* dimg,
+                                       float* colsum, int beta_cs, void* ws, int64_t ws_bytes, int R, int D) {
+  hipStream_t s = (hipStream_t)stream;
+  CLIPMI_REQUIRE(ln_fast_width(D), "layernorm_bwd_x3: D / 64 must be one of 1, 2, 3, 4, 6, 8, 12, 16");
+  CLIPMI_REQUIRE(dy && x && mean && rstd && w && dx && dw && db && dimg && colsum, "layernorm_bwd_x3: arguments");
+  CLIPMI_REQUIRE(ws && ws_bytes >= clipmi_layernorm_bwd_x3_ws(R, D) && ((uintptr_t)ws & 15) == 0 &&
+                     ((uintptr_t)dimg & 7) == 0,
+                 "layernorm_bwd_x3: workspace (clipmi_layernorm_bwd_x3_ws, 16-byte aligned), dimg 8-byte aligned");
+  if (R == 0) return CLIPMI_OK;
+  int nb = (R + 3) / 4;
+  if (nb > 1024) nb = 1024;
+  float* wsf = (float*)ws;
+  LN_DISPATCH(D, ln_bwd_x3_launch, float, float, s, nb, dy, lddy, x, ldx, mean, rstd, w, dx, lddx, dres, ldres, wsf, R,
+              D, dimg);
+  CLIPMI_CHECK_LAUNCH();
+  DeferredReduce r;
+  memset(&r, 0, sizeof(r));
+  r.kind = 2;
+  r.part = wsf; r.stride = (int64_t)3 * D; r.P = nb; r.D = D; r.out = dw; r.out2 = db; r.pbeta = beta_wb;
+  CLIPMI_TRY(launch_partials_reduce(s, r));
+  r.part = wsf + 2 * D; r.out = colsum; r.out2 = nullptr; r.pbeta = beta_cs;
+  CLIPMI_TRY(launch_partials_reduce(s, r));
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
 }
