@@ -272,6 +272,10 @@ int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, float* lse, 
                             int causal, int B, int H, int N, int D);
 int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void* o, const float* lse, const void* dout,
                             void* dqkv, const int64_t* attention_mask, int causal, int B, int H, int N, int D);
+/* clipmi_attention_fwd_x3 that also writes O's pattern-0 split image oimg bf16 [B*N][3D] (8-byte aligned) beside the
+   fp32 O: the out-projection's operand in the bf16x3 engine without a split pass.  N <= 288. */
+int clipmi_attention_fwd_x3img(void* stream, const void* qkv, void* o, void* oimg, float* lse,
+                               const int64_t* attention_mask, int causal, int B, int H, int N, int D);
 /* clipmi_attention_bwd_x3 with d_qkv written as its pattern-1 split image dimg bf16 [B*N][9D] (the layout of
    clipmi_split3_colsum) and d_qkv's column sums (the q / k / v bias gradient) added onto colsum[3D] (+= when beta),
    instead of the fp32 dqkv; N <= 288, ws >= clipmi_attention_bwd_x3img_ws(B, D) bytes, 256-byte aligned. */

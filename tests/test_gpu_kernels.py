@@ -203,6 +203,12 @@ def test_attention_bwd_x3img_matches_fp32_then_split(B, N, H, causal):
            img.data_ptr(), cs.data_ptr(), 1, ws.data_ptr(), ws.numel(), mp, int(causal), B, H, N, D)
     assert torch.equal(img, _split_ref(dqkv, 1))
     assert rel(cs - cs0, dqkv.double().sum(0)) < 1e-5
+    # the forward's image form: O and lse unchanged, O's pattern-0 image beside them
+    o2, lse2 = torch.empty_like(o), torch.empty_like(lse)
+    oimg = torch.full((B * N, 3 * D), float("nan"), dtype=torch.bfloat16, device="cuda")
+    T.call("clipmi_attention_fwd_x3img", s, qkv.data_ptr(), o2.data_ptr(), oimg.data_ptr(), lse2.data_ptr(), mp,
+           int(causal), B, H, N, D)
+    assert torch.equal(o2, o) and torch.equal(lse2, lse) and torch.equal(oimg, _split_ref(o, 0))
     with pytest.raises(ValueError, match="N <= 288"):
         T.call("clipmi_attention_bwd_x3img", s, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(),
                img.data_ptr(), cs.data_ptr(), 1, ws.data_ptr(), ws.numel(), mp, int(causal), 1, H, 300, D)

@@ -150,6 +150,7 @@ _lib.declare("clipmi_layernorm_fwd_x3", [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c
                                          ctypes.c_float])
 _lib.declare("clipmi_attention_fwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd_x3", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
+_lib.declare("clipmi_attention_fwd_x3img", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int])
 _lib.declare("clipmi_attention_bwd_x3img_ws", [c_int, c_int], c_i64)
 _lib.declare("clipmi_attention_bwd_x3img", [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_vp, c_int,
                                             c_int, c_int, c_int, c_int])

@@ -38,11 +38,13 @@ struct AttnX {
   // image output of the backward (clipmi_attention_bwd_x3img): d_qkv as its pattern-1 split image [B*N][9D] and the
   // per-batch-row column sums of d_qkv colp[B][3D] (the qkv bias gradient's partials)
   bf16* dimg; float* colp;
+  // forward (clipmi_attention_fwd_x3img): O's pattern-0 image [B*N][3D] beside the fp32 O, or null
+  bf16* oimg;
 };
 
 // four fp32 values of an output row -> the pattern-1 image segments (h, l, h) at row + c, + seg, + 2 seg, with the
 // rounding of clipmi_split3_colsum (no contraction of v - h into a producing multiply)
-__device__ __forceinline__ void st_x3_4(bf16* row, int64_t seg, int c, const float v[4]) {
+__device__ __forceinline__ void st_x3_4(bf16* row, int64_t seg, int c, const float v[4], bool p1 = true) {
 #pragma clang fp contract(off)
   bf16x4 h, l;
 #pragma unroll
@@ -51,8 +53,8 @@ __device__ __forceinline__ void st_x3_4(bf16* row, int64_t seg, int c, const flo
     l[j] = (bf16)(v[j] - (float)h[j]);
   }
   *(bf16x4*)(row + c) = h;
-  *(bf16x4*)(row + seg + c) = l;
-  *(bf16x4*)(row + 2 * seg + c) = h;
+  *(bf16x4*)(row + seg + c) = p1 ? l : h;
+  *(bf16x4*)(row + 2 * seg + c) = p1 ? h : l;
 }
 
 // sum of v over the 16 row lanes (li) of each lane group g, added by lane li == 0 into red[c .. c + 3]
@@ -223,10 +225,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_x3(AttnX p, int causal) {
       if (q[j] < N) {
         const float inv = lsum[j] > 0.f ? 1.f / lsum[j] : 0.f;
         float* orow = p.o + ((int64_t)b * N + q[j]) * D + h * 64;
+        bf16* irow = p.oimg ? p.oimg + ((int64_t)b * N + q[j]) * 3 * D + h * 64 : nullptr;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           float w[4] = {acc[j][v][0] * inv, acc[j][v][1] * inv, acc[j][v][2] * inv, acc[j][v][3] * inv};
           store4(orow + v * 16 + 4 * g, w);
+          if (irow) st_x3_4(irow, D, v * 16 + 4 * g, w, false);
         }
         if (g == 0)
           p.lse[((int64_t)b * p.H + h) * N + q[j]] = lsum[j] > 0.f ? (mref[j] + __log2f(lsum[j])) * LN2 : NEG_INF;
@@ -556,8 +560,9 @@ extern "C" int clipmi_attention_bwd(void*, int, const void*, const void*, const 
 
 // fp32 q/k/v [B*N, 3D] -> fp32 O [B*N, D] + lse, products as bf16x3 split MFMAs (N > 288: the exact-f32
 // kernels of clipmi_attention_fwd).  Same arguments and outputs as clipmi_attention_fwd with dtype fp32.
-extern "C" int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, float* lse,
-                                       const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
+namespace {
+int attention_fwd_x3(void* stream, const void* qkv, void* o, void* oimg, float* lse, const int64_t* attention_mask,
+                     int causal, int B, int H, int N, int D) {
   hipStream_t s = (hipStream_t)stream;
   CLIPMI_REQUIRE(D == H * 64, "head_dim must be 64");
   CLIPMI_REQUIRE(N >= 1, "N >= 1");
@@ -565,7 +570,8 @@ extern "C" int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, f
   if (N > X3_MAX_N) return clipmi_attention_fwd(stream, CLIPMI_F32, qkv, o, lse, attention_mask, causal, B, H, N, D);
   if (B == 0) return CLIPMI_OK;
   CLIPMI_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)o & 15) == 0, "qkv / o must be 16-byte aligned");
-  AttnX p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f, nullptr, nullptr};
+  AttnX p{(const float*)qkv, (float*)o, lse, attention_mask, nullptr, nullptr, B, H, N, D, 0.125f, nullptr, nullptr,
+          (bf16*)oimg};
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 4.0 * B * H * (double)N * npad * 64;  // the MFMA work issued: three products each
   ProfScope ps(s, "attn_fwd_x3", flops);
@@ -573,6 +579,20 @@ extern "C" int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, f
   ps.finish("attn_fwd_x3", flops);
   CLIPMI_CHECK_LAUNCH();
   return CLIPMI_OK;
+}
+}  // namespace
+
+extern "C" int clipmi_attention_fwd_x3(void* stream, const void* qkv, void* o, float* lse,
+                                       const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
+  return attention_fwd_x3(stream, qkv, o, nullptr, lse, attention_mask, causal, B, H, N, D);
+}
+// the same with O's pattern-0 split image written beside the fp32 O (oimg bf16 [B*N][3D], 8-byte aligned): the
+// out-projection's operand without a split pass.  N <= 288.
+extern "C" int clipmi_attention_fwd_x3img(void* stream, const void* qkv, void* o, void* oimg, float* lse,
+                                          const int64_t* attention_mask, int causal, int B, int H, int N, int D) {
+  CLIPMI_REQUIRE(N >= 1 && N <= X3_MAX_N, "attention_fwd_x3img: 1 <= N <= 288");
+  CLIPMI_REQUIRE(oimg && ((uintptr_t)oimg & 7) == 0, "attention_fwd_x3img: oimg 8-byte aligned");
+  return attention_fwd_x3(stream, qkv, o, oimg, lse, attention_mask, causal, B, H, N, D);
 }
 
 // the backward of clipmi_attention_fwd_x3 (fp32 dO in, fp32 dq / dk / dv out into dqkv [B*N, 3D])
@@ -590,7 +610,7 @@ extern "C" int clipmi_attention_bwd_x3(void* stream, const void* qkv, const void
                      ((uintptr_t)dqkv & 15) == 0,
                  "qkv / o / dout / dqkv must be 16-byte aligned");
   AttnX p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, (float*)dqkv, B, H, N, D,
-          0.125f, nullptr, nullptr};
+          0.125f, nullptr, nullptr, nullptr};
   const size_t lds = bwd_x3_lds(N);
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 10.0 * B * H * (double)N * npad * 64;
@@ -634,7 +654,7 @@ extern "C" int clipmi_attention_bwd_x3img(void* stream, const void* qkv, const v
   if (B == 0) return CLIPMI_OK;
   float* colp = (float*)ws;
   AttnX p{(const float*)qkv, (float*)o, (float*)lse, attention_mask, (const float*)dout, nullptr, B, H, N, D, 0.125f,
-          (bf16*)dimg, colp};
+          (bf16*)dimg, colp, nullptr};
   const size_t lds = bwd_x3_lds(N);
   const int npad = (N + 31) & ~31;
   const double flops = 3 * 10.0 * B * H * (double)N * npad * 64;

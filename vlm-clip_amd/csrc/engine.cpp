@@ -312,8 +312,13 @@ int encoder_fwd_x3(void* s, const clipmi_encoder_desc* d) {
     CLIPMI_TRY(clipmi_layernorm_fwd_x3(s, (const float*)a.x_in, D, a.ln1, 0, (const float*)w.ln1_w,
                                        (const float*)w.ln1_b, a.mean1, a.rstd1, R, D, d->eps));
     CLIPMI_TRY(x3_fwd(s, wimg, R, 3 * D, D, a.ln1, w.qkv_w, a.qkv, 3 * D, CLIPMI_EPI_BIAS, w.qkv_b));
-    CLIPMI_TRY(clipmi_attention_fwd_x3(s, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
-    CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)a.o, D, R, D, o3, 0, nullptr, 0, nullptr, 0));
+    if (d->N <= 288) {  // O and its image from the attention kernel
+      CLIPMI_TRY(clipmi_attention_fwd_x3img(s, a.qkv, a.o, o3, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N,
+                                            D));
+    } else {
+      CLIPMI_TRY(clipmi_attention_fwd_x3(s, a.qkv, a.o, a.lse, d->attention_mask, d->causal, d->B, d->H, d->N, D));
+      CLIPMI_TRY(clipmi_split3_colsum(s, (const float*)a.o, D, R, D, o3, 0, nullptr, 0, nullptr, 0));
+    }
     CLIPMI_TRY(x3_fwd(s, wimg, R, D, D, o3, w.out_w, a.h, D, CLIPMI_EPI_BIAS | CLIPMI_EPI_RESID, w.out_b, a.x_in, D));
     CLIPMI_TRY(clipmi_layernorm_fwd_x3(s, (const float*)a.h, D, a.ln2, 0, (const float*)w.ln2_w,
                                        (const float*)w.ln2_b, a.mean2, a.rstd2, R, D, d->eps));
