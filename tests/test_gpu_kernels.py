@@ -845,14 +845,18 @@ def test_split3_colsum_and_layernorm_x3(R, N, pattern):
         assert torch.equal(y3, _split_ref(y, pattern)) and torch.equal(st, st3)
 
 
-@pytest.mark.parametrize("R", [600, 520, 777])
-def test_gemm_x3out_writes_the_split_image(R):
+@pytest.mark.parametrize("R,K,w4", [(600, 256, "1"), (520, 256, "1"), (777, 256, "1"), (777, 512, "1"),
+                                    (777, 512, "0")])
+def test_gemm_x3out_writes_the_split_image(R, K, w4, monkeypatch):
     """clipmi_gemm_x3out (the bf16x3 mode's fc1 forward and fc2 input gradient since round 6): the epilogue writes the
     split image of its fp32 result instead of the result -- equal to the fp32-output product split afterwards
     (clipmi_split3_colsum's rounding), with fc1's fp32 derivative beside it and the pattern-1 product's column sums
-    (the bias gradient) added onto colsum.  R = 520 / 777: partial 256-row tiles, one with a wave wholly past M."""
+    (the bias gradient) added onto colsum.  R = 520 / 777: partial 256-row tiles, one with a wave wholly past M.
+    Kernels: K' = 3K = 768 runs fc1 on the 8-wave kernel and fc2's input gradient on the persistent 4-wave one,
+    K' = 1536 both on the 4-wave kernel, or both on the 8-wave one with CLIPMI_GEMM_X3_W4=0."""
     from clipmi import _lib
-    K, N = 256, 384
+    monkeypatch.setenv("CLIPMI_GEMM_X3_W4", w4)
+    N = 384
     s = kern.stream()
     x = rnd((R, K), 31, torch.float32)
     w = rnd((N, K), 32, torch.float32) * 0.05
@@ -875,7 +879,7 @@ def test_gemm_x3out_writes_the_split_image(R):
     # h + l keeps ~16 of fp32's 24 bits (2^-17 relative); the image is bit for bit the split of the fp32 product
     mh = (img[:, :N] != ref[:, :N]).float().mean().item()
     ml = (img[:, 2 * N:] != ref[:, 2 * N:]).float().mean().item()
-    print(f"\n[x3out fc1 R={R}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, y) {rel(hl, y):.2e}")
+    print(f"\n[x3out fc1 R={R} K={K} w4={w4}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, y) {rel(hl, y):.2e}")
     assert rel(hl, y) < 2e-5 and torch.equal(img, ref)
     assert rel(dact2, dact) < 1e-6
     # fc2's input gradient: d_pre = (dy W2) * dact, pattern 1, bias gradient of fc1 from its column sums
@@ -899,7 +903,7 @@ def test_gemm_x3out_writes_the_split_image(R):
     gref = _split_ref(g, 1)
     mh = (gimg[:, :N] != gref[:, :N]).float().mean().item()
     ml = (gimg[:, N:2 * N] != gref[:, N:2 * N]).float().mean().item()
-    print(f"[x3out fc2 dgrad R={R}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, g) {rel(hl, g):.2e}")
+    print(f"[x3out fc2 dgrad R={R} K={K} w4={w4}] h mismatch {mh:.2e}, l mismatch {ml:.2e}, rel(h + l, g) {rel(hl, g):.2e}")
     assert rel(hl, g) < 2e-5 and torch.equal(gimg, gref)
     assert rel(cs - cs0, g.double().sum(0)) < 1e-5
     cs1 = torch.zeros(N, device="cuda")

@@ -1197,6 +1197,13 @@ constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QG
 constexpr int E_P = CLIPMI_EPI_STORE_PRE, E_DQ = CLIPMI_EPI_DQGELU, E_DG = CLIPMI_EPI_DGELU, E_BETA = CLIPMI_EPI_BETA;
 constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
 
+// the bf16x3 image-output products (clipmi_gemm_x3out, K' = 3K >= 2304) on the persistent 4-wave kernel; 0: the
+// 8-wave kernel (CLIPMI_GEMM_X3_W4=0, A/B; read per call)
+bool w4_x3() {
+  const char* e = getenv("CLIPMI_GEMM_X3_W4");
+  return !(e && e[0] == '0');
+}
+
 const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, int sel, int flags, float* bg) {
   if (sel == 0 && (p.ws || (f32o && flags == E_BETA))) {
     if (p.var == 28 || p.var == 32) {  // the persistent 4-wave kernel (gemm4.hip; 32: with the L2 prefetch)
@@ -1236,7 +1243,7 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
   // fp32 output of a bf16 product (the bf16 mode's fp32 residual stream: out-projection and fc2 with the
   // residual fused; the patch embedding; the bf16x3 split products): the same kernels, fp32 epilogue
   if (f32o && !p.ws && splits == 1 && sel == 3) {
-    if ((w4_default || p.var == 28) && (flags == E_B || flags == (E_B | E_R) || flags == 0)) {
+    if ((w4_default || p.var == 28) && (flags == E_B || flags == (E_B | E_R) || flags == 0 || (p.x3o && w4_x3()))) {
       if (const char* l = dispatch_w4_f32(p, s, flags, true)) return l;
     }
     switch (flags) {
@@ -1252,7 +1259,7 @@ const char* dispatch256(const GemmP& p, int splits, hipStream_t s, bool f32o, in
   // the bf16x3 mode's input gradients (fp32 gradients; fc2's with the stored-derivative product); the plain
   // ones (K' = 3K >= 2304) on the persistent 4-wave kernel, whose long-K main loop is the faster one
   if (f32o && !p.ws && splits == 1 && sel == 2) {
-    if ((w4_default || p.var == 28) && flags == 0) {
+    if ((w4_default || p.var == 28) && (flags == 0 || (p.x3o && w4_x3()))) {
       if (const char* l = dispatch_w4_f32(p, s, flags, false)) return l;
     }
     switch (flags) {

@@ -1019,11 +1019,27 @@ const char* dispatch_w4(const GemmP& p, hipStream_t s, bool bkm, int flags, int 
 // fp32-output forward products (k-major B) on the persistent kernel: the bf16 mode's fp32 residual stream
 // (fc2 with bias + residual) and fp32-output bf16 products
 const char* dispatch_w4_f32(const GemmP& p, hipStream_t s, int flags, bool bkm) {
-  constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID;
-  if (!bkm) {  // the bf16x3 mode's plain input gradients (K' = 3K >= 2304), fp32 out
+  constexpr int E_B = CLIPMI_EPI_BIAS, E_R = CLIPMI_EPI_RESID, E_Q = CLIPMI_EPI_QGELU;
+  constexpr int E_DA = CLIPMI_EPI_STORE_DACT, E_MA = CLIPMI_EPI_MUL_AUX;
+  if (!bkm) {  // the bf16x3 mode's input gradients (K' = 3K >= 2304), fp32 out or (fc2's, x3o) the image
+    if (flags == E_MA && p.x3o) {
+      launch_w4p<true, false, float, E_MA, false>(p, 1, s, nullptr);
+      return "gemm256_dgrad_mulaux_f32";
+    }
     if (flags != 0) return nullptr;
     launch_w4p<true, false, float, 0, false>(p, 1, s, nullptr);
     return "gemm256_dgrad_f32";
+  }
+  if (p.x3o) {  // the bf16x3 mode's fc1 writing its activation's image (clipmi_gemm_x3out)
+    if (flags == (E_B | E_Q | E_DA)) {
+      launch_w4p<true, true, float, E_B | E_Q | E_DA, false>(p, 1, s, nullptr);
+      return "gemm256_fwd_bias_qgelu_dact_f32";
+    }
+    if (flags == (E_B | E_Q)) {
+      launch_w4p<true, true, float, E_B | E_Q, false>(p, 1, s, nullptr);
+      return "gemm256_fwd_bias_qgelu_f32";
+    }
+    return nullptr;
   }
   switch (flags) {
     case E_B | E_R: launch_w4p<true, true, float, E_B | E_R, false>(p, 1, s, nullptr); return "gemm256_fwd_bias_resid_f32";

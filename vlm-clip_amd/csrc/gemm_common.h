@@ -752,7 +752,7 @@ __device__ __forceinline__ void epilogue_lds_pipe(const GemmP& p, f32x4 (&acc)[N
 // colp[(mb >> 7) * N + n] (rows in order per lane, then a fixed xor tree over the 16 row lanes: deterministic).
 // Register layout as epilogue256_w: after v_permlane16_swap lane (q, mlane) holds row mb + 16 i + mlane, columns
 // nb + 32 jp + coff .. + 7.  N % 8 == 0, ldc % 8 == 0, C 16-B aligned, aux fp32 16-B aligned (host-checked).
-template <int EPI>
+template <int EPI, bool AR = false>
 __device__ __forceinline__ void epilogue_x3img(const GemmP& p, f32x4 (&acc)[8][4], int mb, int nb, int lane) {
   // no fma contraction: l = bf16(v - h) of the ROUNDED v (a contracted v * s - h would split the unrounded product
   // and differ from clipmi_split3_colsum's image of the stored fp32 result in l's last bit for ~1 % of elements)
@@ -806,6 +806,8 @@ __device__ __forceinline__ void epilogue_x3img(const GemmP& p, f32x4 (&acc)[8][4
       for (int jp = 0; jp < 2; ++jp) {
         const int n = nb + 32 * jp + coff;
         float v[8], w2[8];
+        // AGPR accumulators (4-wave kernel): a scheduling fence per fragment pair, as epilogue_lds_pipe
+        if constexpr (AR) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
@@ -876,10 +878,10 @@ __device__ __forceinline__ void finish256(const GemmP& p, f32x4 (&acc)[8][4], in
   // bf16x3 image output (clipmi_gemm_x3out): the fp32-output instances of fc1 (bias + quick_gelu, with or
   // without the stored derivative) and of fc2's input gradient (the stored-derivative product)
   constexpr int X3E = EPI & ~CLIPMI_EPI_STORE_DACT;
-  if constexpr (std::is_same<OutT, float>::value && !AR &&
+  if constexpr (std::is_same<OutT, float>::value &&
                 (X3E == (CLIPMI_EPI_BIAS | CLIPMI_EPI_QGELU) || EPI == CLIPMI_EPI_MUL_AUX)) {
     if (p.x3o) {
-      epilogue_x3img<EPI>(p, acc, mb, nb, lane);
+      epilogue_x3img<EPI, AR>(p, acc, mb, nb, lane);
       return;
     }
   }
