@@ -114,8 +114,8 @@ FAMILIES_FP32 = {"gemm_f32": ["gemm_f32"]}  # --precision fp32: every GEMM is th
 PEAKS = {"gemm_fp8": PEAK_FP8_TFLOPS, "gemm_f32": PEAK_FP32_TFLOPS}
 # HBM traffic per launch of each family, from rocprofv3 --pmc passes (tools/traffic_pmc.sh); named
 # explicitly so the file read is the one committed for this build, not the newest on disk
-TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r05_traffic_fwd_dgrad.json",
-                 "gemm256_wgrad": "profiles/r05_traffic_wgrad.json",
+TRAFFIC_FILES = {"gemm256_fwd_dgrad": "profiles/r06_traffic_fwd_dgrad.json",
+                 "gemm256_wgrad": "profiles/r06_traffic_wgrad.json",
                  "attention": "profiles/r05_traffic_attention.json"}
 
 
