@@ -591,15 +591,16 @@ def test_fp8_rejects_training_towers():
 _ATOMIC_GRADS = ("token_embedding.weight",)
 
 
-@pytest.mark.parametrize("freeze", [True, False])
-def test_deterministic_replay(freeze):
+@pytest.mark.parametrize("freeze,precision", [(True, "bf16"), (False, "bf16"), (False, "bf16x3")])
+def test_deterministic_replay(freeze, precision):
     """SURVEY §5 race check: the same step twice on the same inputs.  Logits and loss must be
     bitwise equal, and so must every gradient but the token embedding's (summed by fp32 atomics:
-    within rounding); a racy kernel shows up as a bitwise difference here."""
+    within rounding); a racy kernel shows up as a bitwise difference here.  bf16x3: the producers that
+    write split images and bias-gradient column partials (GEMM epilogues, attention and LayerNorm backwards)."""
     runs = []
     for _ in range(2):
         m = CLIPWithAdapters("B/32", freeze_clip=freeze, use_shared_adapters=False, device="cuda",
-                             precision="bf16", init_seed=3)
+                             precision=precision, init_seed=3)
         b = batch(m.config, 64)
         out = m(**b, return_loss=True)
         out["loss"].backward()
@@ -618,7 +619,7 @@ def test_deterministic_replay(freeze):
         if any(k in n for k in _ATOMIC_GRADS) and d < 1e-5:
             continue
         racy.append((n, d))
-    print(f"\n[replay freeze={freeze}] {len(g0)} gradients, not bitwise equal beyond atomics: {racy[:8]}")
+    print(f"\n[replay freeze={freeze} {precision}] {len(g0)} gradients, not bitwise equal beyond atomics: {racy[:8]}")
     assert not racy, racy
 
 
