@@ -635,6 +635,40 @@ def test_adapter_fused_pooled_rows_matches_torch(dtype, R, D, A, ln):
         assert rel(gr[k] - grads0[k], ref[k].grad) < (tol if dtype == torch.float32 else 5e-2), k
 
 
+@pytest.mark.parametrize("R,D,A", [(1024, 768, 256), (1000, 1024, 256), (33, 512, 512), (1, 512, 64), (300, 768, 128)])
+def test_adapter_fwd_fused_kernel_matches_sequence(R, D, A, monkeypatch):
+    """The bf16 adapter forward as one kernel (adapter_fused.hip: down GEMM + gelu, up GEMM + residual and the
+    LayerNorm's row statistics as wavefront reductions in one workgroup) against the launch sequence it replaces
+    (CLIPMI_ADAPTER_FUSED=0: down GEMM, up GEMM, LayerNorm): the same MFMA k-order, epilogue arithmetic and
+    LayerNorm summation order, so pre / act / z / y / mean / rstd agree bit for bit (y and the statistics up to a
+    last-bit difference in the odd element)."""
+    g = torch.Generator().manual_seed(R + D + A + 7)
+    mk = lambda *sh, sc=1.0: (torch.randn(*sh, generator=g) * sc).cuda().to(torch.bfloat16)
+    names = ["down.weight", "down.bias", "up.weight", "up.bias", "ln.weight", "ln.bias"]
+    sd = {"down.weight": mk(A, D, sc=D ** -0.5), "down.bias": mk(A, sc=0.1), "up.weight": mk(D, A, sc=A ** -0.5),
+          "up.bias": mk(D, sc=0.1), "ln.weight": mk(D, sc=0.2) + 1, "ln.bias": mk(D, sc=0.1)}
+    x = mk(R, D)
+    s = kern.stream()
+    outs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CLIPMI_ADAPTER_FUSED", fused)
+        y = torch.empty(R, D, dtype=torch.bfloat16, device="cuda")
+        pre, act = (torch.empty(R, A, dtype=torch.bfloat16, device="cuda") for _ in range(2))
+        z = torch.empty(R, D, dtype=torch.bfloat16, device="cuda")
+        st = torch.empty(2, R, device="cuda")
+        T.call("clipmi_adapter_fwd", s, BF16, R, D, A, x.data_ptr(), D, *(sd[k].data_ptr() for k in names), 1e-5, 1,
+               y.data_ptr(), D, pre.data_ptr(), act.data_ptr(), z.data_ptr(), st[0].data_ptr(), st[1].data_ptr())
+        torch.cuda.synchronize()
+        outs[fused] = (pre, act, z, y, st)
+    (p1, a1, z1, y1, s1), (p0, a0, z0, y0, s0) = outs["1"], outs["0"]
+    neq = {k: int((u != v).sum()) for k, (u, v) in {"pre": (p1, p0), "act": (a1, a0), "z": (z1, z0), "y": (y1, y0),
+                                                     "stats": (s1, s0)}.items()}
+    print(f"\n[adapter fused vs sequence R={R} D={D} A={A}] differing elements {neq}")
+    assert torch.equal(p1, p0) and torch.equal(a1, a0) and torch.equal(z1, z0)
+    assert rel(y1, y0) < 1e-3 and rel(s1, s0) < 1e-6
+    assert neq["y"] <= max(1, y1.numel() // 1000)
+
+
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 4, False), (3, 300, 2, True), (1, 1000, 2, False)])
 def test_attention_fwd_mxfp8_output(B, N, H, causal):
     """clipmi_attention_fwd_mxfp8 (config 5's out-projection operand straight from the streaming

@@ -19,6 +19,7 @@
 //             dx = d_pre W_down + dz                                (residual fused)
 // Every launch is enqueued on the caller's stream, in this order; no host synchronisation.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include "internal.h"
 
@@ -79,6 +80,17 @@ extern "C" int clipmi_adapter_fwd(void* stream, int dtype, int R, int D, int A, 
                  "adapter_fwd: act (and z, mean, rstd with the LayerNorm) are required: they carry the bottleneck "
                  "activation, the pre-LN sum and its statistics between the launches");
   if (R == 0) return CLIPMI_OK;
+  // bf16 with the LayerNorm: the one-kernel form (adapter_fused.hip) where it measured faster than the sequence
+  // (D <= 512: 37.5 vs 38.9 us at R = 1024; D = 768 / 1024: 48 / 59 vs 43 / 46 us, its per-workgroup phases being
+  // latency chains at these row counts; profiles/r06_adapter_fused_ab.log).  Bitwise equal either way;
+  // CLIPMI_ADAPTER_FUSED=1 / 0 forces the fused kernel / the sequence (A/B).
+  const char* fe = getenv("CLIPMI_ADAPTER_FUSED");
+  const bool want = fe ? fe[0] == '1' : D <= 512;
+  const uintptr_t al16 = (uintptr_t)x | (uintptr_t)w_down | (uintptr_t)w_up | (uintptr_t)b_down | (uintptr_t)b_up |
+                         (uintptr_t)ln_w | (uintptr_t)ln_b;
+  if (want && adapter_fused_ok(dtype, ln, D, A, ldx, ldy) && (al16 & 15) == 0 && ((uintptr_t)y & 7) == 0)
+    return adapter_fwd_fused(stream, R, D, A, x, ldx, w_down, b_down, w_up, b_up, ln_w, ln_b, eps, y, ldy, pre, act, z,
+                             mean, rstd);
   const int f_down = CLIPMI_EPI_BIAS | CLIPMI_EPI_GELU | (pre ? CLIPMI_EPI_STORE_PRE : 0);
   CLIPMI_TRY(adp_gemm(stream, dtype, R, A, D, x, ldx, true, w_down, D, true, act, A, dtype, f_down, b_down, nullptr, 0,
                       pre, A));

@@ -71,3 +71,8 @@ int launch_partials_reduce(hipStream_t s, const DeferredReduce& r);  // kind 2 (
 // column sums from P partial rows [P][N] (+= when beta), deterministic; fold: 64 x N floats (gemm.hip)
 int colsum_partials_finish(hipStream_t s, const float* part, int P, int N, float* colsum, int beta, float* fold);
 int64_t colsum_partials_ws(int P, int N);  // bytes for the partial rows (256-B aligned) + fold
+// the adapter's fused forward (adapter_fused.hip): whether it covers a call, and the kernel
+bool adapter_fused_ok(int dtype, int ln, int D, int A, int64_t ldx, int64_t ldy);
+int adapter_fwd_fused(void* stream, int R, int D, int A, const void* x, int64_t ldx, const void* w_down,
+                      const void* b_down, const void* w_up, const void* b_up, const void* ln_w, const void* ln_b,
+                      float eps, void* y, int64_t ldy, void* pre, void* act, void* z, float* mean, float* rstd);
