@@ -591,6 +591,37 @@ def test_fp8_rejects_training_towers():
 _ATOMIC_GRADS = ("token_embedding.weight",)
 
 
+def test_bf16x3_long_sequence_backward_matches_fp32():
+    """bf16x3 with more than 288 vision tokens (N = 325: past the x3 attention kernels' LDS limit), so the engine
+    takes its fallback branches -- the exact-f32 attention and the split passes over O and d_qkv -- beside the fused
+    image producers (fc1 / fc2's input gradient, LayerNorm backwards): loss, logits and every gradient against the
+    exact-f32 mode on the same weights and batch (the x3 error model: ~2^-16 per product)."""
+    cfg = C.CLIPConfig(C._text(128, 256, 2, 2, vocab_size=1000, eos_token_id=999, bos_token_id=998),
+                       C._vision(128, 256, 2, 2, 8, image=144), 64, name="long")
+    res = {}
+    for precision in ("fp32", "bf16x3"):
+        m = CLIPWithAdapters(cfg, use_text_adapter=False, use_vision_adapter=False, use_shared_adapters=False,
+                             freeze_clip=False, device="cuda", precision=precision)
+        assert m.config.vision_config.num_positions > 288
+        out = m(**batch(m.config, 8), return_loss=True)
+        out["loss"].backward()
+        torch.cuda.synchronize()
+        res[precision] = (out["loss"].item(), out["logits_per_text"].detach().float().clone(),
+                          {n: p.grad.detach().double().clone() for n, p in m.named_parameters() if p.grad is not None})
+        del m, out
+    (l0, z0, g0), (l1, z1, g1) = res["fp32"], res["bf16x3"]
+    gmax = max(float(v.abs().max()) for v in g0.values())
+    worst = max((float((g1[n] - v).abs().max()) / max(float(v.abs().max()), 0.05 * gmax, 1e-6), n)
+                for n, v in g0.items())
+    dz = float((z1 - z0).abs().max())
+    print(f"\n[bf16x3 N=325 vs fp32] |dloss| {abs(l1 - l0):.2e}, max|dlogit| {dz:.2e}, worst grad err {worst[0]:.2e} "
+          f"at {worst[1]}")
+    # measured: |dloss| 1e-6, max|dlogit| 1.2e-4, worst gradient 1.6e-4 (layer 0's fc2 weight); bounds with >= 3x
+    # headroom: the logits at north_star's 1e-3, the gradients at 5e-4 of the tensor's (or 5 % of the largest) scale
+    assert abs(l1 - l0) < 3e-5 and dz < 1e-3
+    assert g0.keys() == g1.keys() and worst[0] < 5e-4, worst
+
+
 @pytest.mark.parametrize("freeze,precision", [(True, "bf16"), (False, "bf16"), (False, "bf16x3")])
 def test_deterministic_replay(freeze, precision):
     """SURVEY §5 race check: the same step twice on the same inputs.  Logits and loss must be
