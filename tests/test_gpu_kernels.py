@@ -365,8 +365,13 @@ def test_im2col_matches_conv(dtype, H, P):
     Kc = 3 * P * P
     Kp = (Kc + 63) // 64 * 64 if Kc % 8 else Kc
     X = torch.empty(B * (G * G + 1), Kp, dtype=dtype, device="cuda")
+    X.fill_(7.0)  # every element must be written (pad columns and the class-token rows as zeros)
     T.call("clipmi_im2col", kern.stream(), DT[dtype], px.data_ptr(), X.data_ptr(), B, 3, H, P, Kp)
     assert X[:, Kc:].abs().max().item() == 0 if Kp > Kc else True
+    # element for element: torch's unfold of the same pixels (a zero row per image for the class token)
+    ref_x = F.unfold(px, P, stride=P).transpose(1, 2).to(dtype)  # [B, G*G, 3*P*P]
+    Xv = X.view(B, G * G + 1, Kp)
+    assert torch.equal(Xv[:, 1:, :Kc], ref_x) and Xv[:, 0].abs().max().item() == 0
     out = torch.empty(B * (G * G + 1), D, dtype=torch.float32, device="cuda")
     Wd = F.pad(W.to(dtype).view(D, Kc), (0, Kp - Kc)).contiguous()
     kern.gemm(B * (G * G + 1), D, Kp, X, Kp, True, Wd, Kp, True, out, D)

@@ -9,6 +9,7 @@
 #include "common.h"
 #include "internal.h"
 #include <cmath>
+#include <type_traits>
 
 namespace {
 
@@ -55,6 +56,53 @@ __global__ __launch_bounds__(256) void im2col8_kernel(const float* px, T* X, int
   T* dst = X + row * Kp + k;
   store4(dst, v);
   store4(dst + 4, v + 4);
+}
+
+// P = 14 (ViT-L/14; K = 588): one thread per (token row, channel, kernel row) -- 14 consecutive pixels of one image
+// row in seven 8-B loads, written as 14 consecutive elements of the im2col row in seven pair stores -- and a 43rd
+// thread per row zeroing the padded columns K .. Kp.  The scalar kernel moved one element per thread with its index
+// divisions (ViT-L/14@336, B = 4096: 6.4 ms).  Even H, 8-B aligned pixels, even Kp (host-checked).
+template <typename T>
+__global__ __launch_bounds__(256) void im2col14_kernel(const float* px, T* X, int64_t rows, int C, int Hh, int G,
+                                                       int K, int Kp) {
+  const int per = C * 14 + 1;
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = id / per;
+  if (row >= rows) return;
+  const int w = (int)(id - row * per);
+  T* dst = X + row * Kp;
+  if (w == C * 14) {
+    for (int k = K; k < Kp; k += 2) {
+      dst[k] = (T)0.f;
+      dst[k + 1] = (T)0.f;
+    }
+    return;
+  }
+  const int Np1 = G * G + 1;
+  const int b = (int)(row / Np1), t = (int)(row - (int64_t)b * Np1);
+  const int c = w / 14, ky = w - c * 14;
+  float v[14];
+#pragma unroll
+  for (int j = 0; j < 14; ++j) v[j] = 0.f;
+  if (t > 0) {
+    const int p = t - 1, gy = p / G, gx = p - gy * G;
+    const float* src = px + (((int64_t)b * C + c) * Hh + gy * 14 + ky) * Hh + gx * 14;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const float2 a = *(const float2*)(src + 2 * j);
+      v[2 * j] = a.x;
+      v[2 * j + 1] = a.y;
+    }
+  }
+  T* o = dst + c * 196 + ky * 14;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    if constexpr (std::is_same<T, float>::value) {
+      *(float2*)(o + 2 * j) = make_float2(v[2 * j], v[2 * j + 1]);
+    } else {
+      *(bf16x2*)(o + 2 * j) = bf16x2{(bf16)v[2 * j], (bf16)v[2 * j + 1]};
+    }
+  }
 }
 
 // The input step fused into patch-embed: decoded uint8 images, channels
@@ -244,6 +292,14 @@ extern "C" int clipmi_im2col(void* stream, int dtype, const float* pixels, void*
     const unsigned nb = (unsigned)((n + 255) / 256);
     if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(im2col8_kernel<bf16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (bf16*)X, rows, C, H, P, G, K, Kp);
     else hipLaunchKernelGGL(im2col8_kernel<float>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (float*)X, rows, C, H, P, G, K, Kp);
+    CLIPMI_CHECK_LAUNCH();
+    return CLIPMI_OK;
+  }
+  if (P == 14 && H % 2 == 0 && Kp % 2 == 0 && ((uintptr_t)pixels & 7) == 0 && ((uintptr_t)X & 7) == 0) {
+    const int64_t n = rows * (C * 14 + 1);
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    if (dtype == CLIPMI_BF16) hipLaunchKernelGGL(im2col14_kernel<bf16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (bf16*)X, rows, C, H, G, K, Kp);
+    else hipLaunchKernelGGL(im2col14_kernel<float>, dim3(nb), dim3(256), 0, (hipStream_t)stream, pixels, (float*)X, rows, C, H, G, K, Kp);
     CLIPMI_CHECK_LAUNCH();
     return CLIPMI_OK;
   }
